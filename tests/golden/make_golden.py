@@ -1,0 +1,212 @@
+"""Generate the committed golden fixtures from the REFERENCE itself (run once, in the build container).
+
+    python tests/golden/make_golden.py
+
+Reads /root/reference (read-only) through tests/golden/_refload.py, which AST-extracts the model
+classes and ``generate_signals`` without executing the training / dataset scripts.  Writes:
+
+* ``inputs.npz``            — noisy/clean spectra made by the reference generator
+                              (数据集产生.py:5-64, ``np.random.seed(20250410)``), float32 as
+                              ``RamanDataset`` casts them (RRCDNet/train.py:38-39).
+* ``model_<Arch>.npz``      — per network: state_dict key list/shapes (the drop-in contract),
+                              reference fp32 CPU outputs on ``inputs.npz`` for synthetic weights
+                              (``oracle.weights.synth_state_dict(seed=1234)``), and for the briefly
+                              trained networks (RRCDNet, DenoiseCNN, PIDN) also the trained weights and outputs.
+* ``metrics.npz``           — per-spectrum MSE/SSIM/Smoothness/Peak2Peak computed by the reference
+                              metric functions (*/evaulate.py:14-21) and scikit-image 0.18.3
+                              (``/opt/conda/bin/python3.9``) on (clean, denoised) pairs.
+* ``generator_stats.json``  — summary statistics of 1000 reference-generated spectra for the
+                              statistical generator tests.
+
+Nothing at test time reads /root/reference; only these data files are committed.
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+
+import _refload  # noqa: E402
+from oracle.weights import synth_state_dict  # noqa: E402
+
+SEED_DATA = 20250410
+SEED_W = 1234
+ARCHS = ["DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN"]
+TRAINED = ["RRCDNet", "DenoiseCNN", "PIDN"]
+# 64->64 conv gain of the synthetic weights: keeps the deep residual stacks finite and the Sigmoid
+# heads out of saturation (measured output std 0.02-0.6 at these settings).
+GAIN = {"DenoiseCNN": 1.0, "RRCDNet": 1.0, "DSDN": 0.7, "ADSDN": 1.0, "PIDN": 0.85, "APIDN": 0.85}
+EDGE_L = [7, 8, 33, 1000]
+
+
+def make_inputs(gen):
+    np.random.seed(SEED_DATA)
+    clean, noisy, snrs, nstd = gen(3, signal_length=10000)
+    out = {"main_noisy": noisy.astype(np.float32), "main_clean": clean.astype(np.float32),
+           "main_clean64": clean, "main_noisy64": noisy}
+    for L in EDGE_L:
+        c, n, _, _ = gen(2, signal_length=L, extreme_noise_prob=0.0 if L <= 100 else 0.05)
+        out[f"edge{L}_noisy"] = n.astype(np.float32)
+        out[f"edge{L}_clean"] = c.astype(np.float32)
+    c, n, _, _ = gen(1, signal_length=16384)
+    out["long_noisy"] = n.astype(np.float32)
+    out["long_clean"] = c.astype(np.float32)
+    return out
+
+
+def input_sets(inp):
+    sets = {"main": inp["main_noisy"]}
+    for L in EDGE_L:
+        sets[f"edge{L}"] = inp[f"edge{L}_noisy"]
+    sets["long"] = inp["long_noisy"]
+    return sets
+
+
+def train_briefly(cls, gen, steps=300, L=1000, batch=8, lr=1e-3):
+    """A short deterministic CPU Adam run so that the weights (and BN stats) look trained."""
+    torch.manual_seed(0)
+    np.random.seed(7)
+    clean, noisy, _, _ = gen(96, signal_length=L)
+    xc = torch.tensor(clean, dtype=torch.float32).unsqueeze(1)
+    xn = torch.tensor(noisy, dtype=torch.float32).unsqueeze(1)
+    model = cls()
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    g = torch.Generator().manual_seed(0)
+    model.train()
+    t0 = time.time()
+    for step in range(steps):
+        idx = torch.randint(0, xn.shape[0], (batch,), generator=g)
+        opt.zero_grad()
+        loss = torch.nn.functional.mse_loss(model(xn[idx]), xc[idx])
+        loss.backward()
+        opt.step()
+    print(f"  trained {cls.__name__}: {steps} steps, final loss {loss.item():.5f}, {time.time()-t0:.1f}s")
+    model.eval()
+    return {k: v.detach().clone() for k, v in model.state_dict().items()}
+
+
+@torch.no_grad()
+def ref_outputs(cls, sd, sets):
+    m = cls()
+    m.load_state_dict(sd, strict=True)
+    m.eval()
+    return {name: m(torch.from_numpy(x).unsqueeze(1)).squeeze(1).numpy().astype(np.float32)
+            for name, x in sets.items()}
+
+
+def gen_stats(gen):
+    np.random.seed(SEED_DATA)
+    clean, noisy, snrs, nstd = gen(1000)
+    seg_counts = np.zeros(41, np.int64)
+    for row in clean:
+        change = np.flatnonzero(np.diff(row) != 0) + 1
+        bounds = np.concatenate([[0], change, [row.size]])
+        runs = np.diff(bounds)[:-1]          # drop the (possibly truncated) last run
+        np.add.at(seg_counts, runs[runs <= 40], 1)
+    resid = noisy - clean
+    spiked = []
+    for r, s in zip(resid, nstd[:, 0]):
+        big = np.abs(r) > 4.0 * s
+        # a spike is >= 20 consecutive points beyond 4 sigma (amplitude >= 5 sigma)
+        run = np.convolve(big.astype(np.int32), np.ones(20, np.int32), mode="valid")
+        spiked.append(bool((run == 20).any()))
+    return {
+        "n": int(clean.shape[0]), "L": int(clean.shape[1]),
+        "seg_len_counts": seg_counts[1:].tolist(),
+        "snr": snrs[:, 0].tolist(),
+        "noise_std_quantiles": np.quantile(nstd[:, 0], [0.0, 0.1, 0.5, 0.9, 1.0]).tolist(),
+        "power_mean": float(np.mean(np.mean(clean ** 2, axis=1))),
+        "spiked_fraction": float(np.mean(spiked)),
+        "row_min_max": [float(clean.min(axis=1).max()), float(clean.max(axis=1).min())],
+    }
+
+
+METRIC_SCRIPT = r'''
+import ast, sys, numpy as np
+from skimage.metrics import structural_similarity as ssim
+src = open(sys.argv[1], encoding="utf-8").read()
+tree = ast.parse(src)
+keep = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name.startswith("compute_")]
+ns = {"np": np}
+exec(compile(ast.Module(body=keep, type_ignores=[]), sys.argv[1], "exec"), ns)
+d = np.load(sys.argv[2])
+clean, den = d["clean"], d["den"]
+out = np.empty((clean.shape[0], 4), np.float64)
+for i, (c, y) in enumerate(zip(clean, den)):
+    out[i] = [ns["compute_mse"](y, c), ssim(c, y, data_range=c.max() - c.min()),
+              ns["compute_smoothness"](y), ns["compute_peak_to_peak"](y)]
+np.save(sys.argv[3], out)
+'''
+
+
+def metric_goldens(clean, den):
+    """Run the reference metric functions + skimage 0.18.3 in the python3.9 env."""
+    with tempfile.TemporaryDirectory() as td:
+        np.savez(os.path.join(td, "in.npz"), clean=clean, den=den)
+        script = os.path.join(td, "m.py")
+        with open(script, "w") as fh:
+            fh.write(METRIC_SCRIPT)
+        subprocess.run(["/opt/conda/bin/python3.9", script,
+                        os.path.join(_refload.REF, "RRCDNet", "evaulate.py"),
+                        os.path.join(td, "in.npz"), os.path.join(td, "out.npy")], check=True,
+                       stderr=subprocess.DEVNULL)
+        return np.load(os.path.join(td, "out.npy"))
+
+
+def main():
+    torch.set_num_threads(os.cpu_count())
+    gen = _refload.load_generate_signals()
+    inp = make_inputs(gen)
+    np.savez_compressed(os.path.join(HERE, "inputs.npz"), **inp)
+    sets = input_sets(inp)
+    trained_outputs = {}
+    for arch in ARCHS:
+        cls = _refload.load_model_class(arch)
+        tmpl_sd = cls().state_dict()
+        keys = list(tmpl_sd.keys())
+        template = {k: (tuple(v.shape), v.dtype) for k, v in tmpl_sd.items()}
+        rec = {"keys": np.array(json.dumps(keys)),
+               "shapes": np.array(json.dumps([list(v.shape) for v in tmpl_sd.values()])),
+               "dtypes": np.array(json.dumps([str(v.dtype) for v in tmpl_sd.values()]))}
+        sd = synth_state_dict(template, SEED_W, GAIN[arch])
+        rec["synth_gain"] = np.array(GAIN[arch])
+        for name, y in ref_outputs(cls, sd, sets).items():
+            rec[f"synth_{name}"] = y
+        if arch in TRAINED:
+            tsd = train_briefly(cls, gen)
+            for k, v in tsd.items():
+                rec[f"w::{k}"] = v.numpy()
+            outs = ref_outputs(cls, tsd, sets)
+            for name, y in outs.items():
+                rec[f"trained_{name}"] = y
+            trained_outputs[arch] = outs["main"]
+        np.savez_compressed(os.path.join(HERE, f"model_{arch}.npz"), **rec)
+        print(f"{arch}: {len(keys)} keys; out range main "
+              f"[{rec['synth_main'].min():.3f}, {rec['synth_main'].max():.3f}]")
+
+    # metric goldens: trained-RRCDNet denoised outputs + noisy-as-denoised + a smooth candidate
+    clean64 = inp["main_clean64"]
+    dens = [trained_outputs["RRCDNet"], inp["main_noisy"],
+            np.clip(inp["main_noisy"], 0, 1).astype(np.float32)]
+    clean_rep = np.concatenate([clean64] * len(dens))
+    den_rep = np.concatenate(dens).astype(np.float32)
+    m = metric_goldens(clean_rep, den_rep)
+    np.savez_compressed(os.path.join(HERE, "metrics.npz"), clean=clean_rep, den=den_rep, per_spectrum=m)
+    print("metrics golden:", m[:3])
+
+    with open(os.path.join(HERE, "generator_stats.json"), "w") as fh:
+        json.dump(gen_stats(gen), fh)
+    print("done")
+
+
+if __name__ == "__main__":
+    main()
