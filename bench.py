@@ -1,0 +1,156 @@
+"""Headline benchmark: denoised spectra/s of the fused RRCDNet forward on MI355X (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--arch RRCDNet] [--dtype bf16] [--batch B]
+
+One step = one forward of the fused network over a batch of B synthetic spectra per GPU (L = 10000),
+generated on-device by the engine's simulator BEFORE the timed region (inputs resident in HBM).
+Data-parallel over N GPUs, one process per GPU (torch.distributed.run): every rank simulates its
+own spectrum-index range, so per-GPU work is fixed as N grows ("weak" scaling); the only
+collective is the end-of-run metric all-reduce (outside the timed region), plus the timing
+barrier/max.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fiber-raman-intensity_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "denoised spectra/sec (node) RRCDNet bf16/fp32 at 1/2/4/8 GPU; % MFMA peak"
+# Dense MFMA peaks, MI355X_MICROARCH.md §Chip-level parameters (spec values)
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
+# conv layer counts per network: (64->64 convs, stems, heads) — SURVEY.md §2 table
+LAYERS = {"DenoiseCNN": (18, 1, 1), "RRCDNet": (29, 2, 2), "DSDN": (32, 1, 1), "PIDN": (30, 1, 1),
+          "ADSDN": (32, 1, 1), "APIDN": (30, 1, 1)}
+SA_CONVS = {"ADSDN": 17, "APIDN": 15}
+
+
+def flops_per_spectrum(arch, L):
+    """Algorithmic FLOPs: sum over Conv1d layers of 2*Cin*Cout*K*L."""
+    big, stems, heads = LAYERS[arch]
+    per_pos = big * 2 * 64 * 64 * 3 + stems * 2 * 64 * 3 + heads * 2 * 64 * 3 + SA_CONVS.get(arch, 0) * 2 * 2 * 7
+    return per_pos * L
+
+
+def cpu_baseline(arch, L, seconds):
+    """The CPU oracle (fp32 PyTorch-CPU restatement, pinned to the reference by the golden
+    fixtures) in the reference evaluate loop shape: batch-1 forwards (evaulate.py:29-32)."""
+    from oracle.models import forward as oracle_forward
+    import raman_mi355x as R
+    torch.manual_seed(0)
+    sd = R.MODELS[arch]().state_dict()
+    x = torch.rand(1, 1, L)
+    oracle_forward(arch, sd, x)                  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        oracle_forward(arch, sd, torch.rand(1, 1, L))
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 3:
+            break
+    return {"value": n / el, "unit": "spectra/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} batch-1 fp32 {arch} forwards at L={L} ({el:.1f} s, oracle.models on "
+                      f"{torch.get_num_threads()} threads, loop shape of evaulate.py:29-32)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--arch", default="RRCDNet")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--batch", type=int, default=8192, help="spectra per GPU per step")
+    ap.add_argument("--L", type=int, default=10000)
+    ap.add_argument("--seed", type=int, default=20250410)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import raman_mi355x as R
+    from raman_mi355x import engine
+
+    torch.manual_seed(1234)                       # random-init weights of the architecture
+    model = R.MODELS[args.arch]().to(dev).eval().set_engine_dtype(args.dtype)
+    B, L = args.batch, args.L
+    clean, noisy, _, _ = engine.generate(B, args.seed, first_index=rank * B, signal_length=L, device=dev)
+    x = noisy.view(B, 1, L)
+    y = torch.empty_like(x)
+    packed = model.packed_weights(dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        engine.forward(args.arch, args.dtype, packed, x, out=y)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps      # one fused kernel launch per step
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # evaluation metrics of the last step, all-reduced across ranks (RCCL over xGMI) — untimed
+    _, sums = engine.metrics(y.view(B, L), clean)
+    if world > 1:
+        dist.all_reduce(sums)
+    sums = sums.cpu().tolist()
+
+    if rank == 0:
+        total = world * B * args.steps
+        fl = flops_per_spectrum(args.arch, L) * B              # per launch
+        achieved = fl / (kernel_ms * 1e-3) / 1e12
+        peak = PEAK_TFLOPS[args.dtype]
+        rec = {
+            "metric": METRIC, "value": total / elapsed, "unit": "spectra/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (on-device simulator, 数据集产生.py contract; random-init weights)",
+            "config": {"workload": f"{args.arch} {args.dtype} fused forward, on-device simulator inputs "
+                                   "(BASELINE.json configs[2])",
+                       "arch": args.arch, "signal_length": L, "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": None,
+                         "kernel_ms": kernel_ms, "flops_per_launch": fl},
+            "metrics_mean": {k: sums[i] / sums[4] for i, k in enumerate(["MSE", "SSIM", "Smoothness", "Peak2Peak"])},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(args.arch, L, args.cpu_seconds)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,155 @@
+// C ABI (include/raman_mi355x.h): argument checking, error reporting and dispatch.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <exception>
+#include <string>
+
+#include "../../include/raman_mi355x.h"
+#include "common.hpp"
+#include "netspec.hpp"
+
+namespace rdn {
+std::string pack(int arch, int dtype, const float* const* tensors, const int64_t* numels, int n, void* dst, size_t cap);
+size_t packed_bytes(const std::vector<Op>& spec, int dtype);
+hipError_t launch_fused_bf16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
+hipError_t launch_fused_f32(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
+hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
+                               void* ws, size_t ws_bytes, hipStream_t s);
+size_t cbam_workspace_bytes(int arch, int dtype, int64_t n, int64_t L);
+hipError_t launch_generate(uint64_t seed, uint64_t first, int64_t n, int L, float snr_lo, float snr_hi, float extreme_prob,
+                           int max_repeat, float* clean, float* noisy, float* snr, float* nstd, hipStream_t s);
+hipError_t launch_metrics(const float* y, const float* clean, int64_t n, int L, double* per, double* sums, hipStream_t s);
+}  // namespace rdn
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return RDN_OK;
+  return fail(RDN_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+bool valid_arch(int a) { return a >= RDN_DENOISECNN && a <= RDN_APIDN; }
+bool valid_dtype(int d) { return d == RDN_F32 || d == RDN_BF16; }
+bool is_cbam(int a) { return a == RDN_ADSDN || a == RDN_APIDN; }
+
+}  // namespace
+
+#define RDN_GUARD_BEGIN try {
+#define RDN_GUARD_END                                     \
+  }                                                       \
+  catch (const std::exception& ex) {                      \
+    return fail(RDN_EINVAL, std::string("exception: ") + ex.what()); \
+  }                                                       \
+  catch (...) {                                           \
+    return fail(RDN_EINVAL, "unknown exception");         \
+  }
+
+extern "C" {
+
+int rdn_version(void) { return RDN_ABI_VERSION; }
+
+const char* rdn_last_error(void) { return g_err.c_str(); }
+
+int rdn_param_names(int arch, char* buf, size_t cap, size_t* needed) {
+  RDN_GUARD_BEGIN
+  if (!valid_arch(arch)) return fail(RDN_EINVAL, "unknown arch " + std::to_string(arch));
+  std::string all;
+  for (const std::string& s : rdn::param_names(rdn::net_spec(arch))) {
+    all += s;
+    all += '\n';
+  }
+  if (needed) *needed = all.size() + 1;
+  if (buf && cap) {
+    const size_t n = all.size() + 1 <= cap ? all.size() + 1 : cap;
+    std::memcpy(buf, all.c_str(), n);
+    buf[n - 1] = '\0';
+    if (n < all.size() + 1) return fail(RDN_ESIZE, "buffer too small for parameter names");
+  }
+  return RDN_OK;
+  RDN_GUARD_END
+}
+
+int rdn_packed_size(int arch, int dtype, size_t* bytes) {
+  RDN_GUARD_BEGIN
+  if (!valid_arch(arch) || !valid_dtype(dtype) || !bytes) return fail(RDN_EINVAL, "rdn_packed_size: bad argument");
+  *bytes = rdn::packed_bytes(rdn::net_spec(arch), dtype);
+  return RDN_OK;
+  RDN_GUARD_END
+}
+
+int rdn_pack(int arch, int dtype, const float* const* tensors, const int64_t* numels, int n_tensors, void* dst,
+             size_t cap) {
+  RDN_GUARD_BEGIN
+  if (!valid_arch(arch) || !valid_dtype(dtype) || !tensors || !numels || !dst || n_tensors < 0)
+    return fail(RDN_EINVAL, "rdn_pack: bad argument");
+  const std::string err = rdn::pack(arch, dtype, tensors, numels, n_tensors, dst, cap);
+  if (!err.empty()) {
+    const bool shape = err.find("expected") != std::string::npos || err.find("tensors") != std::string::npos;
+    return fail(err.find("too small") != std::string::npos ? RDN_ESIZE : shape ? RDN_ESHAPE : RDN_EINVAL, err);
+  }
+  return RDN_OK;
+  RDN_GUARD_END
+}
+
+int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes) {
+  RDN_GUARD_BEGIN
+  if (!valid_arch(arch) || !valid_dtype(dtype) || !bytes || n < 0 || L < 1)
+    return fail(RDN_EINVAL, "rdn_workspace_size: bad argument");
+  *bytes = is_cbam(arch) ? rdn::cbam_workspace_bytes(arch, dtype, n, L) : 0;
+  return RDN_OK;
+  RDN_GUARD_END
+}
+
+int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* y, int64_t n, int64_t L, void* ws,
+                size_t ws_bytes, void* stream) {
+  RDN_GUARD_BEGIN
+  if (!valid_arch(arch) || !valid_dtype(dtype)) return fail(RDN_EINVAL, "rdn_forward: unknown arch/dtype");
+  if (!packed || !x || !y) return fail(RDN_EINVAL, "rdn_forward: null pointer");
+  if (n < 0 || L < 1 || L > 0x7fffffff) return fail(RDN_EINVAL, "rdn_forward: need n >= 0 and 1 <= L < 2^31");
+  if (n == 0) return RDN_OK;
+  const hipStream_t s = (hipStream_t)stream;
+  const uint8_t* blob = (const uint8_t*)packed;
+  if (is_cbam(arch)) {
+    const size_t need = rdn::cbam_workspace_bytes(arch, dtype, n, L);
+    if (ws_bytes < need || (need && !ws))
+      return fail(RDN_ESIZE, "rdn_forward: workspace too small, need " + std::to_string(need) + " bytes");
+    return hip_check(rdn::launch_cbam_forward(arch, dtype, blob, x, y, n, (int)L, ws, ws_bytes, s), "cbam forward");
+  }
+  if (dtype == RDN_BF16) return hip_check(rdn::launch_fused_bf16(arch, blob, x, y, n, (int)L, s), "fused bf16 forward");
+  return hip_check(rdn::launch_fused_f32(arch, blob, x, y, n, (int)L, s), "fused f32 forward");
+  RDN_GUARD_END
+}
+
+int rdn_generate(uint64_t seed, uint64_t first_index, int64_t n, const rdn_gen_params* p, float* clean, float* noisy,
+                 float* snr_db, float* noise_std, void* stream) {
+  RDN_GUARD_BEGIN
+  if (!p || !clean || !noisy) return fail(RDN_EINVAL, "rdn_generate: null pointer");
+  if (n < 0 || p->signal_length < 1 || p->signal_length > 0x7fffffff || p->max_repeat < 1 || !(p->snr_hi >= p->snr_lo))
+    return fail(RDN_EINVAL, "rdn_generate: bad parameters");
+  if (n == 0) return RDN_OK;
+  return hip_check(rdn::launch_generate(seed, first_index, n, (int)p->signal_length, p->snr_lo, p->snr_hi,
+                                        p->extreme_noise_prob, p->max_repeat, clean, noisy, snr_db, noise_std,
+                                        (hipStream_t)stream),
+                   "generate");
+  RDN_GUARD_END
+}
+
+int rdn_metrics(const float* y, const float* clean, int64_t n, int64_t L, double* per_spectrum, double* sums,
+                void* stream) {
+  RDN_GUARD_BEGIN
+  if (!y || !clean) return fail(RDN_EINVAL, "rdn_metrics: null pointer");
+  if (n < 0 || L < 7 || L > 0x7fffffff) return fail(RDN_EINVAL, "rdn_metrics: need L >= 7 (SSIM window)");
+  if (n == 0) return RDN_OK;
+  return hip_check(rdn::launch_metrics(y, clean, n, (int)L, per_spectrum, sums, (hipStream_t)stream), "metrics");
+  RDN_GUARD_END
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+// Shared definitions for the gfx950 (MI355X / CDNA4) Raman denoising engine.
+//
+// Everything here describes ONE fused tile: a workgroup owns WB consecutive positions of one
+// spectrum (the tile's output positions plus a halo on each side) and keeps the 64-channel
+// activations of that window in LDS from the first Conv1d to the last.  HBM is touched only for
+// the 1-channel input/output spectrum and the (L2-resident) packed weights.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+// read-only global data through the constant address space: uniform indices become s_load
+typedef __attribute__((address_space(4))) const float cfloat;
+
+namespace rdn {
+
+constexpr int C = 64;            // hidden channels of every network
+constexpr int KT = 3;            // conv taps
+constexpr int WB = 512;          // activation rows (positions) per tile, halo included
+constexpr int GUARD = 2;         // zero rows on each side of a buffer (max dilation)
+constexpr int ROWS = WB + 2 * GUARD;
+constexpr int THREADS = 512;     // 8 waves: 2 per SIMD
+constexpr int WAVES = THREADS / 64;
+
+// ---- packed weight blob -------------------------------------------------------------------
+// [small section: SMALL_SLOTS slots of 256 fp32]  [big section: n_big x BIG_BYTES_<dtype>]
+// small slot = stem  {w[c*3+t] (192), bias[c] (64)}  or  head {w[c*3+t] (192), bias (1), pad}
+//            or CBAM parameters (see cbam.hip).
+constexpr int SMALL_SLOT_FLOATS = 256;
+constexpr int SMALL_SLOTS = 64;
+constexpr size_t SMALL_BYTES = SMALL_SLOTS * SMALL_SLOT_FLOATS * sizeof(float);   // 64 KiB
+// bf16 big layer: A-fragments of v_mfma_f32_16x16x32_bf16, [m 4][kstep 6][lane 64][8 bf16],
+// lane l holds W[cout = 16m + (l&15)][cin = 32u + 8(l>>4) + j][tap t], kstep = 2t + u; then bias[64] f32.
+constexpr int BIG_FRAG_BYTES_BF16 = 4 * 6 * 64 * 16;                       // 24576
+constexpr int BIG_BYTES_BF16 = BIG_FRAG_BYTES_BF16 + C * 4;                // 24832 (1552 x 16 B)
+// f32 big layer: A-operands of v_mfma_f32_16x16x4_f32, [m 4][tg 12][lane 64][i 4] f32,
+// lane l holds W[cout = 16m + (l&15)][cin = 16g + 4(l>>4) + i][tap t], tg = 4t + g; then bias[64].
+constexpr int BIG_FRAG_FLOATS_F32 = 4 * 12 * 64 * 4;                       // 12288
+constexpr int BIG_BYTES_F32 = (BIG_FRAG_FLOATS_F32 + C) * 4;               // 49408
+
+// ---- LDS image ------------------------------------------------------------------------------
+// bf16 activation buffer: ROWS x 128 B, 16-B slots XOR-swizzled by (row & 7): conflict-free
+// ds_read_b128 B-fragment reads for any row offset, 2-way ds_write_b64 epilogue stores.
+constexpr int ROWB_BF16 = C * 2;
+constexpr int ACT_BYTES_BF16 = ROWS * ROWB_BF16;                           // 66048
+// f32 activation buffer: ROWS x 256 B, slots swizzled by 2*(row & 7).
+constexpr int ROWB_F32 = C * 4;
+constexpr int ACT_BYTES_F32 = ROWS * ROWB_F32;                             // 132096
+
+__device__ __forceinline__ uint32_t off_bf16(int prow, int byte) {
+  return (uint32_t)(prow * ROWB_BF16) + ((((byte >> 4) ^ (prow & 7)) << 4) | (byte & 15));
+}
+__device__ __forceinline__ uint32_t off_f32(int prow, int byte) {
+  return (uint32_t)(prow * ROWB_F32) + ((((byte >> 4) ^ ((prow & 7) << 1)) << 4) | (byte & 15));
+}
+
+enum Arch : int { DENOISECNN = 0, RRCDNET = 1, DSDN = 2, ADSDN = 3, PIDN = 4, APIDN = 5 };
+enum DType : int { F32 = 0, BF16 = 1 };
+
+// receptive half-width (rows of halo needed on each side of a tile's outputs)
+__host__ __device__ constexpr int fused_halo(int arch) {
+  return arch == DENOISECNN ? 20 : arch == RRCDNET ? 29 : arch == DSDN ? 34 : arch == PIDN ? 32 : 0;
+}
+
+struct Geometry {       // tiling of one launch
+  int L;                // spectrum length
+  int T;                // output positions per tile (WB - 2*halo)
+  int tiles;            // tiles per spectrum
+  int halo;
+};
+
+}  // namespace rdn

@@ -1,0 +1,304 @@
+// Load-time weight preparation (host): BatchNorm folding + MFMA fragment layout.
+//
+// Replaces the reference's ``model.load_state_dict(torch.load(path))`` (*/evaulate.py:66): the
+// state_dict tensors are consumed in the order of net_spec(), eval-mode BatchNorm1d
+// (y = (x - mean) / sqrt(var + 1e-5) * gamma + beta) is folded into the preceding Conv1d in fp64,
+// and each 64->64 layer is written as the A-operand fragments its kernel loads (common.hpp).
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "netspec.hpp"
+
+namespace rdn {
+
+static constexpr double BN_EPS = 1e-5;
+
+std::vector<Op> net_spec(int arch) {
+  std::vector<Op> s;
+  auto stem = [&](const std::string& c, const std::string& bn, int slot) { s.push_back({OpKind::STEM, c, bn, slot}); };
+  auto big = [&](const std::string& c, const std::string& bn) { s.push_back({OpKind::BIG, c, bn, -1}); };
+  auto head = [&](const std::string& c, int slot) { s.push_back({OpKind::HEAD, c, "", slot}); };
+  auto cbam = [&](const std::string& p, int slot, bool bias, const char* ca, const char* sa) {
+    Op o{OpKind::CBAM, p, "", slot};
+    o.bias = bias;
+    o.ca = ca;
+    o.sa = sa;
+    s.push_back(o);
+  };
+  switch (arch) {
+    case DENOISECNN:                                   // 1DCNN/train.py:74-78
+      stem("layers.0", "", 0);
+      for (int i = 2; i < 20; ++i) big("layers." + std::to_string(i) + ".0", "");
+      head("layers.20", 1);
+      break;
+    case RRCDNET:                                      // RRCDNet/train.py:77-90
+      stem("right_net.0", "right_net.1", 0);
+      for (int i = 3; i < 18; ++i) big("right_net." + std::to_string(i) + ".0", "right_net." + std::to_string(i) + ".1");
+      head("right_net.18", 2);
+      stem("left_net.0", "left_net.1", 1);
+      for (int i = 3; i < 10; ++i) big("left_net." + std::to_string(i) + ".0", "");
+      big("left_net.10", "left_net.11");
+      for (int i = 13; i < 19; ++i) big("left_net." + std::to_string(i) + ".0", "");
+      head("left_net.19", 3);
+      break;
+    case DSDN:                                         // DSDN/train.py:104-118
+      stem("down_sampling.conv", "", 0);
+      big("conv1", "");
+      big("conv2", "");
+      for (int i = 0; i < 15; ++i) {
+        const std::string p = "res_blocks." + std::to_string(i);
+        big(p + ".conv1", p + ".bn1");
+        big(p + ".conv2", p + ".bn2");
+      }
+      head("conv_out", 1);
+      break;
+    case ADSDN:                                        // ADSDN/train.py:151-158
+      stem("down_sampling.conv", "", 0);
+      cbam("down_sampling.cbam", 2, true, "channel_attention", "spatial_attention");
+      big("conv1", "");
+      big("conv2", "");
+      cbam("cbam", 5, true, "channel_attention", "spatial_attention");
+      for (int i = 0; i < 15; ++i) {
+        const std::string p = "res_blocks." + std::to_string(i);
+        big(p + ".conv1", p + ".bn1");
+        big(p + ".conv2", p + ".bn2");
+        cbam(p + ".cbam", 8 + 3 * i, true, "channel_attention", "spatial_attention");
+      }
+      head("conv_out", 1);
+      break;
+    case PIDN:                                         // PIDN/train.py:75-99
+      stem("down_sampling.0", "", 0);
+      for (int i = 0; i < 15; ++i) {
+        const std::string p = "res_blocks." + std::to_string(i);
+        big(p + ".0", p + ".1");
+        big(p + ".3", p + ".4");
+      }
+      head("conv_out.0", 1);
+      break;
+    case APIDN:                                        // APIDN/train.py:122-148
+      stem("down_sampling.0", "", 0);
+      for (int i = 0; i < 15; ++i) {
+        const std::string p = "res_blocks." + std::to_string(i);
+        big(p + ".0", p + ".1");
+        big(p + ".3", p + ".4");
+        cbam(p + ".5", 2 + 3 * i, false, "ca", "sa");
+      }
+      head("conv_out.0", 1);
+      break;
+    default:
+      break;
+  }
+  return s;
+}
+
+static void conv_names(const Op& o, std::vector<std::string>& out) {
+  out.push_back(o.conv + ".weight");
+  out.push_back(o.conv + ".bias");
+  if (!o.bn.empty()) {
+    for (const char* k : {".weight", ".bias", ".running_mean", ".running_var"}) out.push_back(o.bn + k);
+  }
+}
+
+std::vector<std::string> param_names(const std::vector<Op>& spec) {
+  std::vector<std::string> out;
+  for (const Op& o : spec) {
+    if (o.kind != OpKind::CBAM) {
+      conv_names(o, out);
+      continue;
+    }
+    const std::string ca = o.conv + "." + o.ca + ".fc.", sa = o.conv + "." + o.sa + ".conv.";
+    out.push_back(ca + "0.weight");
+    if (o.bias) out.push_back(ca + "0.bias");
+    out.push_back(ca + "2.weight");
+    if (o.bias) out.push_back(ca + "2.bias");
+    out.push_back(sa + "weight");
+    if (o.bias) out.push_back(sa + "bias");
+  }
+  return out;
+}
+
+int big_layers(const std::vector<Op>& spec, int dtype) {
+  int n = 0;
+  for (const Op& o : spec) n += o.kind == OpKind::BIG || (o.kind == OpKind::HEAD && dtype == BF16);
+  return n;
+}
+
+// ---- packing ----------------------------------------------------------------------------------
+
+struct Folded {            // conv weight [cout][cin][3] and bias [cout] after BN folding, fp64
+  int cout, cin;
+  std::vector<double> w, b;
+  double W(int co, int ci, int t) const { return w[((size_t)co * cin + ci) * 3 + t]; }
+};
+
+struct Reader {
+  const float* const* t;
+  const int64_t* numel;
+  int n, i = 0;
+  std::string err;
+  const float* take(const std::string& name, int64_t expect) {
+    if (i >= n) { err = "too few tensors: missing " + name; return nullptr; }
+    if (numel[i] != expect) {
+      err = name + ": expected " + std::to_string(expect) + " elements, got " + std::to_string(numel[i]);
+      return nullptr;
+    }
+    if (!t[i]) { err = name + ": null pointer"; return nullptr; }
+    return t[i++];
+  }
+};
+
+static bool fold(Reader& rd, const Op& o, int cin, int cout, Folded& f) {
+  const float* w = rd.take(o.conv + ".weight", (int64_t)cout * cin * 3);
+  const float* b = w ? rd.take(o.conv + ".bias", cout) : nullptr;
+  if (!b) return false;
+  f.cout = cout;
+  f.cin = cin;
+  f.w.assign(w, w + (size_t)cout * cin * 3);
+  f.b.assign(b, b + cout);
+  if (o.bn.empty()) return true;
+  const float* g = rd.take(o.bn + ".weight", cout);
+  const float* be = g ? rd.take(o.bn + ".bias", cout) : nullptr;
+  const float* mu = be ? rd.take(o.bn + ".running_mean", cout) : nullptr;
+  const float* var = mu ? rd.take(o.bn + ".running_var", cout) : nullptr;
+  if (!var) return false;
+  for (int c = 0; c < cout; ++c) {
+    const double s = (double)g[c] / std::sqrt((double)var[c] + BN_EPS);
+    for (int k = 0; k < cin * 3; ++k) f.w[(size_t)c * cin * 3 + k] *= s;
+    f.b[c] = (f.b[c] - (double)mu[c]) * s + (double)be[c];
+  }
+  return true;
+}
+
+static uint16_t to_bf16(double v) {      // fp64 -> fp32 -> bf16, round to nearest even
+  const float f = (float)v;
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+static void pack_big_bf16(const Folded& f, uint8_t* dst) {
+  uint16_t* frag = (uint16_t*)dst;
+  for (int m = 0; m < 4; ++m)
+    for (int s = 0; s < 6; ++s)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int t = s >> 1, u = s & 1;
+          const int co = 16 * m + (lane & 15), ci = 32 * u + 8 * (lane >> 4) + j;
+          const double v = co < f.cout ? f.W(co, ci, t) : 0.0;
+          frag[(((m * 6 + s) * 64) + lane) * 8 + j] = to_bf16(v);
+        }
+  float* bias = (float*)(dst + BIG_FRAG_BYTES_BF16);
+  for (int c = 0; c < C; ++c) bias[c] = c < f.cout ? (float)f.b[c] : 0.f;
+}
+
+static void pack_big_f32(const Folded& f, uint8_t* dst) {
+  float* frag = (float*)dst;
+  for (int m = 0; m < 4; ++m)
+    for (int tg = 0; tg < 12; ++tg)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int i = 0; i < 4; ++i) {
+          const int t = tg >> 2, g = tg & 3;
+          const int co = 16 * m + (lane & 15), ci = 16 * g + 4 * (lane >> 4) + i;
+          frag[((m * 12 + tg) * 64 + lane) * 4 + i] = (float)f.W(co, ci, t);
+        }
+  float* bias = frag + BIG_FRAG_FLOATS_F32;
+  for (int c = 0; c < C; ++c) bias[c] = (float)f.b[c];
+}
+
+static void pack_small_conv(const Folded& f, float* slot) {   // w[c*3+t], bias at 192 (+c)
+  std::memset(slot, 0, SMALL_SLOT_FLOATS * sizeof(float));
+  if (f.cin == 1) {
+    for (int c = 0; c < f.cout; ++c) {
+      for (int t = 0; t < 3; ++t) slot[3 * c + t] = (float)f.W(c, 0, t);
+      slot[192 + c] = (float)f.b[c];
+    }
+  } else {
+    for (int c = 0; c < f.cin; ++c)
+      for (int t = 0; t < 3; ++t) slot[3 * c + t] = (float)f.W(0, c, t);
+    slot[192] = (float)f.b[0];
+  }
+}
+
+// CBAM: slot+0 fc.0.weight [4][64]; slot+1 fc.2.weight [64][4]; slot+2: fc.0.bias[4] @0,
+// fc.2.bias[64] @4, sa.conv.weight [2][7] @68, sa.conv.bias @82 (zeros when the layer has no bias).
+static bool pack_cbam(Reader& rd, const Op& o, float* small) {
+  const std::string ca = o.conv + "." + o.ca + ".fc.", sa = o.conv + "." + o.sa + ".conv.";
+  float* s0 = small + o.slot * SMALL_SLOT_FLOATS;
+  float* s1 = s0 + SMALL_SLOT_FLOATS;
+  float* s2 = s1 + SMALL_SLOT_FLOATS;
+  std::memset(s0, 0, 3 * SMALL_SLOT_FLOATS * sizeof(float));
+  const float* p;
+  if (!(p = rd.take(ca + "0.weight", 4 * 64))) return false;
+  std::memcpy(s0, p, 256 * sizeof(float));
+  if (o.bias) {
+    if (!(p = rd.take(ca + "0.bias", 4))) return false;
+    std::memcpy(s2, p, 4 * sizeof(float));
+  }
+  if (!(p = rd.take(ca + "2.weight", 64 * 4))) return false;
+  std::memcpy(s1, p, 256 * sizeof(float));
+  if (o.bias) {
+    if (!(p = rd.take(ca + "2.bias", 64))) return false;
+    std::memcpy(s2 + 4, p, 64 * sizeof(float));
+  }
+  if (!(p = rd.take(sa + "weight", 14))) return false;
+  std::memcpy(s2 + 68, p, 14 * sizeof(float));
+  if (o.bias) {
+    if (!(p = rd.take(sa + "bias", 1))) return false;
+    s2[82] = p[0];
+  }
+  return true;
+}
+
+size_t packed_bytes(const std::vector<Op>& spec, int dtype) {
+  return SMALL_BYTES + (size_t)big_layers(spec, dtype) * (dtype == BF16 ? BIG_BYTES_BF16 : BIG_BYTES_F32);
+}
+
+// returns "" on success, else the error message
+std::string pack(int arch, int dtype, const float* const* tensors, const int64_t* numels, int n, void* dst,
+                 size_t cap) {
+  const std::vector<Op> spec = net_spec(arch);
+  if (spec.empty()) return "unknown arch " + std::to_string(arch);
+  if (dtype != F32 && dtype != BF16) return "unknown dtype " + std::to_string(dtype);
+  const size_t need = packed_bytes(spec, dtype);
+  if (cap < need) return "destination too small: need " + std::to_string(need) + " bytes";
+  uint8_t* out = (uint8_t*)dst;
+  std::memset(out, 0, need);
+  float* small = (float*)out;
+  uint8_t* big = out + SMALL_BYTES;
+  const size_t big_bytes = dtype == BF16 ? BIG_BYTES_BF16 : BIG_BYTES_F32;
+  Reader rd{tensors, numels, n};
+  int layer = 0;
+  for (const Op& o : spec) {
+    Folded f;
+    switch (o.kind) {
+      case OpKind::STEM:
+        if (!fold(rd, o, 1, C, f)) return rd.err;
+        pack_small_conv(f, small + o.slot * SMALL_SLOT_FLOATS);
+        break;
+      case OpKind::BIG:
+        if (!fold(rd, o, C, C, f)) return rd.err;
+        if (dtype == BF16) pack_big_bf16(f, big + layer * big_bytes);
+        else pack_big_f32(f, big + layer * big_bytes);
+        ++layer;
+        break;
+      case OpKind::HEAD:
+        if (!fold(rd, o, C, 1, f)) return rd.err;
+        pack_small_conv(f, small + o.slot * SMALL_SLOT_FLOATS);
+        if (dtype == BF16) pack_big_bf16(f, big + (layer++) * big_bytes);
+        break;
+      case OpKind::CBAM:
+        if (!pack_cbam(rd, o, small)) return rd.err;
+        break;
+    }
+  }
+  if (rd.i != n) return "too many tensors: consumed " + std::to_string(rd.i) + " of " + std::to_string(n);
+  return "";
+}
+
+}  // namespace rdn

@@ -1,0 +1,74 @@
+"""ctypes binding of libraman_mi355x.so (the C ABI declared in include/raman_mi355x.h).
+
+torch is imported first on purpose: the library is linked against the HIP runtime that
+PyTorch-ROCm bundles (torch/lib/libamdhip64.so) and must resolve to that already-loaded copy so
+that device pointers and streams are shared with torch.  There is no fallback: if the library is
+missing the import fails loudly.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before the library, see module docstring)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libraman_mi355x.so")
+
+RDN_OK = 0
+ABI_VERSION = 1
+
+c_float_p = ctypes.POINTER(ctypes.c_float)
+c_double_p = ctypes.POINTER(ctypes.c_double)
+
+
+class GenParams(ctypes.Structure):
+    _fields_ = [("signal_length", ctypes.c_int64), ("snr_lo", ctypes.c_float), ("snr_hi", ctypes.c_float),
+                ("extreme_noise_prob", ctypes.c_float), ("max_repeat", ctypes.c_int32)]
+
+
+_SIGNATURES = {
+    "rdn_version": ([], ctypes.c_int),
+    "rdn_last_error": ([], ctypes.c_char_p),
+    "rdn_param_names": ([ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "rdn_packed_size": ([ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "rdn_pack": ([ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
+                  ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t], ctypes.c_int),
+    "rdn_workspace_size": ([ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                            ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "rdn_forward": ([ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
+    "rdn_generate": ([ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, ctypes.POINTER(GenParams), ctypes.c_void_p,
+                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "rdn_metrics": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                     ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+}
+
+EXPORTED = tuple(_SIGNATURES)
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the native library.  Raises ImportError if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"raman_mi355x native library not built: {LIB_PATH} is missing "
+                              "(run `python -c 'import __graft_entry__ as g; g.build()'` or `make -C csrc`)")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.argtypes = args
+            fn.restype = res
+        if handle.rdn_version() != ABI_VERSION:
+            raise ImportError(f"libraman_mi355x ABI {handle.rdn_version()} != expected {ABI_VERSION}")
+        _lib = handle
+    return _lib
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def check(rc, what):
+    if rc != RDN_OK:
+        msg = lib().rdn_last_error().decode(errors="replace")
+        raise EngineError(f"{what} failed (code {rc}): {msg}")

@@ -1,0 +1,139 @@
+"""Thin tensor-level wrappers over the C ABI: weight packing, forward, simulator and metrics.
+
+All compute runs in libraman_mi355x.so on the caller's current HIP stream; these functions only
+check shapes/devices, allocate outputs through the PyTorch caching allocator and pass raw
+pointers.  Nothing here has a CPU or PyTorch-op fallback.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+ARCHS = ("DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN")
+ARCH_ID = {a: i for i, a in enumerate(ARCHS)}
+DTYPE_ID = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}
+
+
+def _arch(arch):
+    if isinstance(arch, int):
+        return arch
+    try:
+        return ARCH_ID[arch]
+    except KeyError:
+        raise ValueError(f"unknown network {arch!r}; expected one of {ARCHS}") from None
+
+
+def _dtype(dtype):
+    if isinstance(dtype, torch.dtype):
+        dtype = {torch.float32: "fp32", torch.bfloat16: "bf16"}.get(dtype, str(dtype))
+    try:
+        return DTYPE_ID[dtype]
+    except KeyError:
+        raise ValueError(f"unknown engine dtype {dtype!r}; expected 'fp32' or 'bf16'") from None
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def param_names(arch):
+    """The state_dict keys the packer consumes, in order (folded BN stats included)."""
+    L = _lib.lib()
+    need = ctypes.c_size_t()
+    _lib.check(L.rdn_param_names(_arch(arch), None, 0, ctypes.byref(need)), "rdn_param_names")
+    buf = ctypes.create_string_buffer(need.value)
+    _lib.check(L.rdn_param_names(_arch(arch), buf, need.value, ctypes.byref(need)), "rdn_param_names")
+    return [s for s in buf.value.decode().split("\n") if s]
+
+
+def packed_size(arch, dtype):
+    n = ctypes.c_size_t()
+    _lib.check(_lib.lib().rdn_packed_size(_arch(arch), _dtype(dtype), ctypes.byref(n)), "rdn_packed_size")
+    return n.value
+
+
+def pack(arch, state_dict, dtype, device):
+    """Fold BN + lay out MFMA fragments on the host, then copy the blob to ``device``."""
+    names = param_names(arch)
+    missing = [k for k in names if k not in state_dict]
+    if missing:
+        raise KeyError(f"state_dict lacks {len(missing)} tensors the engine needs, e.g. {missing[:3]}")
+    host = [state_dict[k].detach().to("cpu", torch.float32).contiguous() for k in names]
+    ptrs = (ctypes.c_void_p * len(host))(*[t.data_ptr() for t in host])
+    numels = (ctypes.c_int64 * len(host))(*[t.numel() for t in host])
+    size = packed_size(arch, dtype)
+    blob = torch.empty(size, dtype=torch.uint8)
+    _lib.check(_lib.lib().rdn_pack(_arch(arch), _dtype(dtype), ptrs, numels, len(host),
+                                   ctypes.c_void_p(blob.data_ptr()), size), "rdn_pack")
+    return blob.to(device)
+
+
+def _check_cuda_f32(t, name):
+    if not (torch.is_tensor(t) and t.is_cuda):
+        raise RuntimeError(f"raman_mi355x runs on the GPU only: {name} must be a CUDA (HIP) tensor")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32, got {t.dtype}")
+
+
+def forward(arch, dtype, packed, x, out=None):
+    """y = Model(x) for x float32 (N, 1, L) (or (N, L)) on the GPU."""
+    _check_cuda_f32(x, "input")
+    if x.dim() == 3 and x.shape[1] != 1:
+        raise ValueError(f"expected (N, 1, L) input, got {tuple(x.shape)}")
+    if x.dim() not in (2, 3):
+        raise ValueError(f"expected (N, 1, L) input, got {tuple(x.shape)}")
+    x = x.contiguous()
+    n, L = x.shape[0], x.shape[-1]
+    y = torch.empty_like(x) if out is None else out
+    if y.shape != x.shape or not y.is_contiguous() or y.device != x.device:
+        raise ValueError("out must be a contiguous tensor like the input")
+    ws_bytes = ctypes.c_size_t()
+    L_ = _lib.lib()
+    _lib.check(L_.rdn_workspace_size(_arch(arch), _dtype(dtype), n, L, ctypes.byref(ws_bytes)), "rdn_workspace_size")
+    ws = torch.empty(ws_bytes.value, dtype=torch.uint8, device=x.device) if ws_bytes.value else None
+    _lib.check(L_.rdn_forward(_arch(arch), _dtype(dtype), ctypes.c_void_p(packed.data_ptr()),
+                              ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), n, L,
+                              ctypes.c_void_p(ws.data_ptr() if ws is not None else 0), ws_bytes.value,
+                              _stream(x.device)), "rdn_forward")
+    return y
+
+
+def generate(n, seed, first_index=0, signal_length=10000, snr_range=(20.0, 37.0), extreme_noise_prob=0.05,
+             max_repeat=40, device="cuda", out=None):
+    """Device simulator (数据集产生.py:5-64 contract): returns clean, noisy (n, L), snr, noise_std (n,)."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        raise RuntimeError("raman_mi355x runs on the GPU only: the simulator needs a CUDA device")
+    L = int(signal_length)
+    if out is None:
+        clean = torch.empty((n, L), dtype=torch.float32, device=device)
+        noisy = torch.empty((n, L), dtype=torch.float32, device=device)
+    else:
+        clean, noisy = out
+    snr = torch.empty(n, dtype=torch.float32, device=device)
+    nstd = torch.empty(n, dtype=torch.float32, device=device)
+    prm = _lib.GenParams(L, float(snr_range[0]), float(snr_range[1]), float(extreme_noise_prob), int(max_repeat))
+    _lib.check(_lib.lib().rdn_generate(int(seed), int(first_index), int(n), ctypes.byref(prm),
+                                       ctypes.c_void_p(clean.data_ptr()), ctypes.c_void_p(noisy.data_ptr()),
+                                       ctypes.c_void_p(snr.data_ptr()), ctypes.c_void_p(nstd.data_ptr()),
+                                       _stream(device)), "rdn_generate")
+    return clean, noisy, snr, nstd
+
+
+def metrics(y, clean, sums=None, per_spectrum=True):
+    """Per-spectrum [MSE, SSIM, Smoothness, Peak2Peak] (fp64, (n, 4)) and accumulated sums (fp64 [5])."""
+    _check_cuda_f32(y, "denoised")
+    _check_cuda_f32(clean, "clean")
+    y = y.reshape(y.shape[0], -1).contiguous()
+    clean = clean.reshape(clean.shape[0], -1).contiguous()
+    if y.shape != clean.shape:
+        raise ValueError(f"shape mismatch {tuple(y.shape)} vs {tuple(clean.shape)}")
+    n, L = y.shape
+    per = torch.empty((n, 4), dtype=torch.float64, device=y.device) if per_spectrum else None
+    if sums is None:
+        sums = torch.zeros(5, dtype=torch.float64, device=y.device)
+    _lib.check(_lib.lib().rdn_metrics(ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(clean.data_ptr()), n, L,
+                                      ctypes.c_void_p(per.data_ptr() if per is not None else 0),
+                                      ctypes.c_void_p(sums.data_ptr()), _stream(y.device)), "rdn_metrics")
+    return per, sums

@@ -1,0 +1,234 @@
+"""Drop-in ``nn.Module`` surfaces of the six reference networks, executed by the HIP engine.
+
+Each class keeps the reference class name, its no-argument constructor and — through an identical
+submodule tree — exactly the reference ``state_dict`` keys, so checkpoints written by
+``torch.save(model.state_dict(), ...)`` in */train.py load with ``strict=True`` and the
+*/evaulate.py flow (``Model().to(DEVICE)``, ``load_state_dict``, ``eval()``, ``model(x)``) runs
+unchanged.  ``forward`` never executes the submodules: on first use (and after any parameter
+change) the state_dict is folded/packed by the native library and the whole network runs as the
+fused gfx950 kernels of ``csrc/``.
+
+Supported: eval mode, CUDA float32 input ``(N, 1, L)``.  Training mode, CPU tensors and
+``requires_grad`` inputs raise (the engine is inference-only).
+"""
+import torch
+import torch.nn as nn
+from torch.nn import init
+
+from . import engine
+
+C = 64
+
+
+def _conv(cin=C, cout=C, dilation=1, bias=True, k=3):
+    return nn.Conv1d(cin, cout, k, padding=dilation * (k // 2), dilation=dilation, bias=bias)
+
+
+def _seq(*mods):
+    return nn.Sequential(*mods)
+
+
+class _EngineNet(nn.Module):
+    """Common engine plumbing: packing cache + forward dispatch."""
+
+    ARCH = None
+
+    def __init__(self):
+        super().__init__()
+        self._engine_dtype = "fp32"
+        self._packed = None
+        self._packed_key = None
+
+    # -- configuration -----------------------------------------------------------------------
+    @property
+    def engine_dtype(self):
+        return self._engine_dtype
+
+    def set_engine_dtype(self, dtype):
+        """'fp32' (exact-fp32 MFMA; 1e-5 parity) or 'bf16' (bf16 MFMA, fp32 accumulate)."""
+        engine._dtype(dtype)
+        self._engine_dtype = "bf16" if dtype in ("bf16", "bfloat16", torch.bfloat16) else "fp32"
+        return self
+
+    # -- packing -----------------------------------------------------------------------------
+    def _state_key(self, device):
+        sd = self.state_dict(keep_vars=True)
+        return (str(device), self._engine_dtype,
+                tuple((t.data_ptr(), t._version) for t in sd.values() if torch.is_tensor(t)))
+
+    def packed_weights(self, device):
+        key = self._state_key(device)
+        if key != self._packed_key:
+            with torch.no_grad():
+                self._packed = engine.pack(self.ARCH, self.state_dict(), self._engine_dtype, device)
+            self._packed_key = key
+        return self._packed
+
+    # -- forward -----------------------------------------------------------------------------
+    def forward(self, x):
+        if self.training:
+            raise RuntimeError(f"{type(self).__name__}: the raman_mi355x engine is inference-only; "
+                               "call model.eval() first (training is out of scope)")
+        if not (torch.is_tensor(x) and x.is_cuda):
+            raise RuntimeError(f"{type(self).__name__}: raman_mi355x runs on the GPU only; move the "
+                               "model input to a CUDA (HIP) device")
+        if torch.is_grad_enabled() and x.requires_grad:
+            raise RuntimeError(f"{type(self).__name__}: autograd is not supported by the engine")
+        if x.dim() != 3 or x.shape[1] != 1:
+            raise ValueError(f"{type(self).__name__}: expected input (N, 1, L), got {tuple(x.shape)}")
+        if x.dtype != torch.float32:
+            raise TypeError(f"{type(self).__name__}: expected float32 input, got {x.dtype}")
+        return engine.forward(self.ARCH, self._engine_dtype, self.packed_weights(x.device), x)
+
+
+def _check_defaults(name, in_channels, num_res_blocks):
+    if in_channels != 1 or num_res_blocks != 15:
+        raise NotImplementedError(f"{name}: the engine's kernels are built for the reference configuration "
+                                  "in_channels=1, num_res_blocks=15")
+
+
+class DenoiseCNN(_EngineNet):
+    """1DCNN/train.py:71-82."""
+
+    ARCH = "DenoiseCNN"
+
+    def __init__(self):
+        super().__init__()
+        body = [_seq(_conv(), nn.ReLU()) for _ in range(18)]
+        self.layers = _seq(_conv(1, C), nn.ReLU(), *body, _conv(C, 1))
+
+
+class RRCDNet(_EngineNet):
+    """RRCDNet/train.py:72-113 (including its Kaiming initialisation, :100-113)."""
+
+    ARCH = "RRCDNet"
+
+    def __init__(self):
+        super().__init__()
+        bn_block = lambda: _seq(_conv(), nn.BatchNorm1d(C), nn.ReLU())   # noqa: E731
+        dil_block = lambda: _seq(_conv(dilation=2), nn.ReLU())           # noqa: E731
+        self.right_net = _seq(_conv(1, C), nn.BatchNorm1d(C), nn.ReLU(),
+                              *[bn_block() for _ in range(15)], _conv(C, 1))
+        self.left_net = _seq(_conv(1, C), nn.BatchNorm1d(C), nn.ReLU(),
+                             *[dil_block() for _ in range(7)],
+                             _conv(), nn.BatchNorm1d(C), nn.ReLU(),
+                             *[dil_block() for _ in range(6)], _conv(C, 1))
+        for mod in self.modules():
+            if isinstance(mod, nn.Conv1d):
+                init.kaiming_normal_(mod.weight, mode="fan_out", nonlinearity="relu")
+                init.zeros_(mod.bias)
+            elif isinstance(mod, nn.BatchNorm1d):
+                init.ones_(mod.weight)
+                init.zeros_(mod.bias)
+
+
+class _ResidualBlock(nn.Module):
+    """DSDN/ADSDN ResidualBlock parameter layout (conv1, bn1, conv2, bn2[, cbam])."""
+
+    def __init__(self, with_cbam=False):
+        super().__init__()
+        self.conv1, self.bn1 = _conv(), nn.BatchNorm1d(C)
+        self.conv2, self.bn2 = _conv(), nn.BatchNorm1d(C)
+        if with_cbam:
+            self.cbam = _CBAM(bias=True, names=("channel_attention", "spatial_attention"))
+
+
+class _Stem(nn.Module):
+    """DownSampling parameter layout: ``conv`` (+ ``cbam`` in ADSDN)."""
+
+    def __init__(self, with_cbam=False):
+        super().__init__()
+        self.conv = _conv(1, C)
+        if with_cbam:
+            self.cbam = _CBAM(bias=True, names=("channel_attention", "spatial_attention"))
+
+
+class _ChannelAttention(nn.Module):
+    def __init__(self, bias):
+        super().__init__()
+        self.avg_pool = nn.AdaptiveAvgPool1d(1)
+        self.max_pool = nn.AdaptiveMaxPool1d(1)
+        self.fc = _seq(nn.Linear(C, C // 16, bias=bias), nn.ReLU(inplace=True), nn.Linear(C // 16, C, bias=bias))
+        self.sigmoid = nn.Sigmoid()
+
+
+class _SpatialAttention(nn.Module):
+    def __init__(self, bias):
+        super().__init__()
+        self.conv = nn.Conv1d(2, 1, 7, padding=3, bias=bias)
+        self.sigmoid = nn.Sigmoid()
+
+
+class _CBAM(nn.Module):
+    """CBAM (ADSDN/train.py:107-116, children channel_attention/spatial_attention, biased) or
+    CBAMBlock (APIDN/train.py:107-116, children ca/sa, bias-free)."""
+
+    def __init__(self, bias, names):
+        super().__init__()
+        setattr(self, names[0], _ChannelAttention(bias))
+        setattr(self, names[1], _SpatialAttention(bias))
+
+
+class DSDN(_EngineNet):
+    """DSDN/train.py:101-126."""
+
+    ARCH = "DSDN"
+
+    def __init__(self, in_channels=1, num_res_blocks=15):
+        super().__init__()
+        _check_defaults("DSDN", in_channels, num_res_blocks)
+        self.down_sampling = _Stem()
+        self.conv1, self.conv2 = _conv(), _conv()
+        self.res_blocks = _seq(*[_ResidualBlock() for _ in range(num_res_blocks)])
+        self.conv_out = _conv(C, in_channels)
+
+
+class ADSDN(_EngineNet):
+    """ADSDN/train.py:150-167."""
+
+    ARCH = "ADSDN"
+
+    def __init__(self, in_channels=1, num_res_blocks=15):
+        super().__init__()
+        _check_defaults("ADSDN", in_channels, num_res_blocks)
+        self.down_sampling = _Stem(with_cbam=True)
+        self.conv1, self.conv2 = _conv(), _conv()
+        self.cbam = _CBAM(bias=True, names=("channel_attention", "spatial_attention"))
+        self.res_blocks = _seq(*[_ResidualBlock(with_cbam=True) for _ in range(num_res_blocks)])
+        self.conv_out = _conv(C, in_channels)
+
+
+def _pidn_block(cbam=False):
+    mods = [_conv(), nn.BatchNorm1d(C), nn.ReLU(), _conv(), nn.BatchNorm1d(C)]
+    if cbam:
+        mods.append(_CBAM(bias=False, names=("ca", "sa")))
+    return _seq(*mods)
+
+
+class PIDN(_EngineNet):
+    """PIDN/train.py:72-106."""
+
+    ARCH = "PIDN"
+
+    def __init__(self, in_channels=1, num_res_blocks=15):
+        super().__init__()
+        _check_defaults("PIDN", in_channels, num_res_blocks)
+        self.down_sampling = _seq(_conv(in_channels, C), nn.ReLU())
+        self.res_blocks = _seq(*[_pidn_block() for _ in range(num_res_blocks)])
+        self.conv_out = _seq(_conv(C, in_channels), nn.Sigmoid())
+
+
+class APIDN(_EngineNet):
+    """APIDN/train.py:119-159."""
+
+    ARCH = "APIDN"
+
+    def __init__(self, in_channels=1, num_res_blocks=15):
+        super().__init__()
+        _check_defaults("APIDN", in_channels, num_res_blocks)
+        self.down_sampling = _seq(_conv(in_channels, C), nn.ReLU())
+        self.res_blocks = nn.ModuleList([_pidn_block(cbam=True) for _ in range(num_res_blocks)])
+        self.conv_out = _seq(_conv(C, in_channels), nn.Sigmoid())
+
+
+MODELS = {cls.ARCH: cls for cls in (DenoiseCNN, RRCDNet, DSDN, ADSDN, PIDN, APIDN)}

@@ -1,0 +1,112 @@
+/*
+ * raman_mi355x — C ABI of the MI355X (gfx950) Raman-denoising inference engine.
+ *
+ * Plain pointers and sizes only: no PyTorch or HIP types cross this boundary (a HIP stream is
+ * passed as `void*`).  Every entry point returns RDN_OK (0) or a negative RDN_E* code and leaves
+ * a message for rdn_last_error() (thread-local).  No exception crosses the ABI.  All device
+ * buffers are owned by the caller (e.g. the PyTorch caching allocator); the library keeps no
+ * device state of its own, enqueues on the caller's stream and never synchronises it.
+ *
+ * Reference interfaces these entry points replace (paths relative to the reference repo):
+ *   rdn_param_names / rdn_packed_size / rdn_pack
+ *       -> Model().load_state_dict(torch.load(path))            <model>/evaulate.py:65-66
+ *          (the reference keeps nn.Module parameters; the engine folds eval-mode BatchNorm and
+ *           re-lays the weights out as MFMA operand fragments once, at load time)
+ *   rdn_forward
+ *       -> Model.forward(x), x float32 (N, 1, L)                   <model>/evaulate.py:30-32, :84-85
+ *          DenoiseCNN 1DCNN/train.py:71-82 · RRCDNet RRCDNet/train.py:72-98 · DSDN DSDN/train.py:101-126
+ *          ADSDN ADSDN/train.py:150-167 · PIDN PIDN/train.py:72-106 · APIDN APIDN/train.py:119-159
+ *   rdn_generate
+ *       -> generate_signals(num_samples, signal_length, snr_range, extreme_noise_prob, max_repeat)
+ *                                                                  数据集产生.py:5-64
+ *   rdn_metrics
+ *       -> compute_mse / compute_smoothness / compute_peak_to_peak + skimage SSIM, averaged
+ *                                                                  <model>/evaulate.py:14-39
+ */
+#ifndef RAMAN_MI355X_H
+#define RAMAN_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RDN_ABI_VERSION 1
+
+typedef enum {
+  RDN_DENOISECNN = 0, /* 1DCNN/train.py   class DenoiseCNN */
+  RDN_RRCDNET = 1,    /* RRCDNet/train.py class RRCDNet    */
+  RDN_DSDN = 2,       /* DSDN/train.py    class DSDN       */
+  RDN_ADSDN = 3,      /* ADSDN/train.py   class ADSDN      */
+  RDN_PIDN = 4,       /* PIDN/train.py    class PIDN       */
+  RDN_APIDN = 5       /* APIDN/train.py   class APIDN      */
+} rdn_arch;
+
+typedef enum { RDN_F32 = 0, RDN_BF16 = 1 } rdn_dtype;
+
+enum {
+  RDN_OK = 0,
+  RDN_EINVAL = -1,       /* bad argument (null pointer, unknown arch/dtype, n or L < 1)      */
+  RDN_EUNSUPPORTED = -2, /* combination not built                                            */
+  RDN_ESHAPE = -3,       /* a tensor handed to rdn_pack has the wrong number of elements      */
+  RDN_ESIZE = -4,        /* destination / workspace buffer too small                          */
+  RDN_EHIP = -5          /* a HIP runtime call failed (message carries hipGetErrorString)     */
+};
+
+/* ABI version (RDN_ABI_VERSION) of the loaded library. */
+int rdn_version(void);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char* rdn_last_error(void);
+
+/* The reference state_dict keys rdn_pack consumes, in order, '\n'-separated, NUL-terminated.
+ * Writes at most `cap` bytes to `buf` (may be NULL with cap 0); `*needed` receives the size. */
+int rdn_param_names(int arch, char* buf, size_t cap, size_t* needed);
+
+/* Bytes of the packed weight blob for (arch, dtype). */
+int rdn_packed_size(int arch, int dtype, size_t* bytes);
+
+/* Fold eval-mode BatchNorm (eps 1e-5) into the preceding Conv1d (in fp64) and lay every layer out
+ * as MFMA operand fragments.  `tensors[i]` is a HOST fp32 pointer to the tensor named by line i
+ * of rdn_param_names (row-major, torch layout), `numels[i]` its element count.  Writes the blob
+ * into host memory `dst` (cap bytes); the caller copies it to the device. */
+int rdn_pack(int arch, int dtype, const float* const* tensors, const int64_t* numels, int n_tensors,
+             void* dst, size_t cap);
+
+/* Device scratch rdn_forward needs for a batch (0 for the fully fused networks). */
+int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes);
+
+/* y[n][L] = Model(x[n][L]) on the device.  x, y: fp32 device pointers (the (N,1,L) tensor is
+ * (N,L) contiguous); packed: device copy of the rdn_pack blob; stream: hipStream_t or NULL. */
+int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* y, int64_t n, int64_t L,
+                void* workspace, size_t workspace_bytes, void* stream);
+
+/* Simulator parameters; defaults of 数据集产生.py:5-7 are {10000, 20, 37, 0.05, 40}. */
+typedef struct {
+  int64_t signal_length;
+  float snr_lo;
+  float snr_hi;
+  float extreme_noise_prob;
+  int32_t max_repeat;
+} rdn_gen_params;
+
+/* Generate spectra first_index .. first_index+n-1 of the stream `seed` (counter-based Philox,
+ * so any index range is reproducible on any device).  clean/noisy: fp32 [n][L] device;
+ * snr_db / noise_std: fp32 [n] device (either may be NULL). */
+int rdn_generate(uint64_t seed, uint64_t first_index, int64_t n, const rdn_gen_params* params,
+                 float* clean, float* noisy, float* snr_db, float* noise_std, void* stream);
+
+/* Per-spectrum MSE, SSIM, Smoothness, Peak2Peak of denoised y against clean (both fp32 [n][L],
+ * device), computed in fp64.  per_spectrum: fp64 [n][4] device (may be NULL).  sums: fp64 [5]
+ * device, ACCUMULATED (+=) as {ΣMSE, ΣSSIM, ΣSmoothness, ΣPeak2Peak, count} (may be NULL).
+ * L must be >= 7 (SSIM window). */
+int rdn_metrics(const float* y, const float* clean, int64_t n, int64_t L, double* per_spectrum,
+                double* sums, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RAMAN_MI355X_H */

@@ -15,8 +15,8 @@ K1, K2 = 0.01, 0.03
 
 
 def _box_mean(a, win=WIN):
-    c = np.concatenate([[0.0], np.cumsum(a, dtype=np.float64)])
-    return (c[win:] - c[:-win]) / win          # mean of a[i : i+win], i = 0 .. L-win
+    """mean of a[i : i+win] for i = 0 .. L-win (direct window sums, no running-sum cancellation)."""
+    return np.lib.stride_tricks.sliding_window_view(a, win).sum(axis=1) / win
 
 
 def ssim_1d(clean, den):

@@ -1,0 +1,118 @@
+"""Parity of the HIP forward against the reference's own outputs (golden fixtures) and the CPU oracle.
+
+Bars (BASELINE.json north_star):
+  fp32: max|y - ref| / max|ref| <= 1e-5
+  bf16: max|y - ref| <= 2e-2 on normalised-intensity outputs (trained weights);
+        for the synthetic weight sets, whose outputs are not normalised, 2e-2 * max(1, max|ref|).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import INPUT_SETS, golden_state_dict, input_array, load_golden
+
+pytestmark = pytest.mark.gpu
+
+FUSED = ["DenoiseCNN", "RRCDNet", "DSDN", "PIDN"]
+TRAINED = ["DenoiseCNN", "RRCDNet", "PIDN"]
+F32_REL = 1e-5
+BF16_ABS = 2e-2
+
+
+def _model(arch, which, dtype):
+    import raman_mi355x as R
+    m = R.MODELS[arch]()
+    m.load_state_dict(golden_state_dict(arch, which), strict=True)
+    return m.cuda().eval().set_engine_dtype(dtype)
+
+
+def _run(m, x_np):
+    x = torch.from_numpy(np.ascontiguousarray(x_np)).unsqueeze(1).cuda()
+    with torch.no_grad():
+        y = m(x)
+    torch.cuda.synchronize()
+    assert y.shape == x.shape and y.dtype == torch.float32
+    return y.squeeze(1).cpu().numpy()
+
+
+def _cases(archs):
+    out = []
+    for a in archs:
+        out.append((a, "synth"))
+        if a in TRAINED:
+            out.append((a, "trained"))
+    return out
+
+
+@pytest.mark.parametrize("arch,which", _cases(FUSED))
+def test_fp32_matches_reference(arch, which, inputs):
+    g = load_golden(arch)
+    m = _model(arch, which, "fp32")
+    for name in INPUT_SETS:
+        ref = g[f"{which}_{name}"]
+        y = _run(m, input_array(inputs, name))
+        rel = np.abs(y - ref).max() / max(np.abs(ref).max(), 1e-30)
+        assert np.isfinite(y).all()
+        assert rel <= F32_REL, f"{arch}/{which}/{name}: fp32 max-rel error {rel:.3e} > {F32_REL}"
+
+
+@pytest.mark.parametrize("arch,which", _cases(FUSED))
+def test_bf16_within_tolerance(arch, which, inputs):
+    g = load_golden(arch)
+    m = _model(arch, which, "bf16")
+    for name in INPUT_SETS:
+        ref = g[f"{which}_{name}"]
+        y = _run(m, input_array(inputs, name))
+        err = np.abs(y - ref).max()
+        tol = BF16_ABS if which == "trained" else BF16_ABS * max(1.0, float(np.abs(ref).max()))
+        print(f"{arch}/{which}/{name}: bf16 max-abs {err:.3e} (tol {tol:.1e})")
+        assert err <= tol, f"{arch}/{which}/{name}: bf16 max-abs error {err:.3e} > {tol:.1e}"
+
+
+@pytest.mark.parametrize("arch", FUSED)
+@pytest.mark.parametrize("L", [1, 2, 5, 453, 454, 455, 908, 2049])
+def test_ragged_lengths_vs_oracle(arch, L):
+    """Tile-boundary and tiny-L cases (T = 512 - 2*halo) against the CPU oracle, fp32."""
+    from oracle.models import forward as oracle_forward
+    sd = golden_state_dict(arch, "synth")
+    m = _model(arch, "synth", "fp32")
+    rng = np.random.default_rng(L)
+    x = rng.uniform(-0.2, 1.2, (3, L)).astype(np.float32)
+    y = _run(m, x)
+    ref = oracle_forward(arch, sd, torch.from_numpy(x).unsqueeze(1)).squeeze(1).numpy()
+    rel = np.abs(y - ref).max() / max(np.abs(ref).max(), 1e-30)
+    assert rel <= F32_REL, f"{arch} L={L}: {rel:.3e}"
+
+
+def test_batch_independence_and_determinism():
+    """Each spectrum's output is independent of its batch neighbours and bitwise reproducible."""
+    m = _model("RRCDNet", "trained", "bf16")
+    rng = np.random.default_rng(0)
+    x = rng.uniform(0, 1, (7, 3000)).astype(np.float32)
+    y_all = _run(m, x)
+    y_again = _run(m, x)
+    y_one = _run(m, x[3:4])
+    assert np.array_equal(y_all, y_again)
+    assert np.array_equal(y_all[3:4], y_one)
+
+
+def test_packing_cache_tracks_weight_updates():
+    m = _model("DenoiseCNN", "synth", "fp32")
+    x = np.random.default_rng(1).uniform(0, 1, (2, 600)).astype(np.float32)
+    y0 = _run(m, x)
+    with torch.no_grad():
+        m.layers[20].bias.add_(1.0)          # head bias: output shifts by exactly 1
+    y1 = _run(m, x)
+    assert np.allclose(y1 - y0, 1.0, atol=1e-5)
+
+
+def test_rejects_unsupported_use():
+    import raman_mi355x as R
+    m = R.RRCDNet().cuda()
+    x = torch.zeros(1, 1, 100, device="cuda")
+    with pytest.raises(RuntimeError):
+        m.train()(x)                      # training mode
+    with pytest.raises(RuntimeError):
+        m.eval()(x.cpu())                 # CPU tensor
+    with pytest.raises(ValueError):
+        m.eval()(torch.zeros(1, 2, 100, device="cuda"))
