@@ -13,7 +13,8 @@ namespace rdn {
 std::string pack(int arch, int dtype, const float* const* tensors, const int64_t* numels, int n, void* dst, size_t cap);
 size_t packed_bytes(const std::vector<Op>& spec, int dtype);
 hipError_t launch_fused_bf16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
-hipError_t launch_fused_f32(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
+hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
+                                hipStream_t s);
 hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                void* ws, size_t ws_bytes, hipStream_t s);
 size_t cbam_workspace_bytes(int arch, int dtype, int64_t n, int64_t L);
@@ -37,7 +38,7 @@ int hip_check(hipError_t e, const char* what) {
 }
 
 bool valid_arch(int a) { return a >= RDN_DENOISECNN && a <= RDN_APIDN; }
-bool valid_dtype(int d) { return d == RDN_F32 || d == RDN_BF16; }
+bool valid_dtype(int d) { return d == RDN_F32 || d == RDN_BF16 || d == RDN_BF16X3; }
 bool is_cbam(int a) { return a == RDN_ADSDN || a == RDN_APIDN; }
 
 }  // namespace
@@ -124,7 +125,7 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
     return hip_check(rdn::launch_cbam_forward(arch, dtype, blob, x, y, n, (int)L, ws, ws_bytes, s), "cbam forward");
   }
   if (dtype == RDN_BF16) return hip_check(rdn::launch_fused_bf16(arch, blob, x, y, n, (int)L, s), "fused bf16 forward");
-  return hip_check(rdn::launch_fused_f32(arch, blob, x, y, n, (int)L, s), "fused f32 forward");
+  return hip_check(rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, s), "fused in-place forward");
   RDN_GUARD_END
 }
 

@@ -38,6 +38,8 @@ constexpr int BIG_FRAG_BYTES_BF16 = 4 * 6 * 64 * 16;                       // 24
 constexpr int BIG_BYTES_BF16 = BIG_FRAG_BYTES_BF16 + C * 4;                // 24832 (1552 x 16 B)
 // f32 big layer: A-operands of v_mfma_f32_16x16x4_f32, [m 4][tg 12][lane 64][i 4] f32,
 // lane l holds W[cout = 16m + (l&15)][cin = 16g + 4(l>>4) + i][tap t], tg = 4t + g; then bias[64].
+// bf16x3 big layer (same size): [m 4][kstep 6][hi/lo 2][lane 64][8 bf16] with the bf16 fragment
+// map above and W = hi + lo; then bias[64] f32.
 constexpr int BIG_FRAG_FLOATS_F32 = 4 * 12 * 64 * 4;                       // 12288
 constexpr int BIG_BYTES_F32 = (BIG_FRAG_FLOATS_F32 + C) * 4;               // 49408
 
@@ -58,7 +60,7 @@ __device__ __forceinline__ uint32_t off_f32(int prow, int byte) {
 }
 
 enum Arch : int { DENOISECNN = 0, RRCDNET = 1, DSDN = 2, ADSDN = 3, PIDN = 4, APIDN = 5 };
-enum DType : int { F32 = 0, BF16 = 1 };
+enum DType : int { F32 = 0, BF16 = 1, BF16X3 = 2 };
 
 // receptive half-width (rows of halo needed on each side of a tile's outputs)
 __host__ __device__ constexpr int fused_halo(int arch) {

@@ -8,9 +8,12 @@
 //   TAG_SCALAR counter 0    : [snr, extreme?, n_spikes, -]
 //   TAG_SPIKE  counter s    : spike s [width, start, amplitude, sign]
 //   TAG_NOISE  counter p>>2 : 4 Box-Muller normals for positions p..p+3
-// Float transforms use explicitly rounded ops (__fmul_rn/__fadd_rn) so that no FMA contraction
-// makes them differ from the float32 numpy restatement.
+// Float transforms are written under `fp contract(off)` (and the file is built with
+// -ffp-contract=off) so that no FMA fusion makes them differ from the float32 numpy restatement.
 #include "common.hpp"
+
+// Every float op below is rounded on its own, exactly like the numpy restatement: no FMA fusion.
+#pragma clang fp contract(off)
 
 namespace rdn {
 namespace gen {
@@ -45,20 +48,20 @@ __device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint
 
 __device__ __forceinline__ float u24(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
 __device__ __forceinline__ float uniform(float lo, float hi, uint32_t x) {
-  return __fadd_rn(lo, __fmul_rn(hi - lo, u24(x)));
+  return lo + (hi - lo) * u24(x);
 }
 __device__ __forceinline__ int randint(int lo, int hi, uint32_t x) {
   return lo + (int)(((uint64_t)x * (uint64_t)(hi - lo)) >> 32);
 }
 __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
-  const float u1 = __fmul_rn((float)(a >> 8) + 1.0f, 1.0f / 16777216.0f);
+  const float u1 = ((float)(a >> 8) + 1.0f) * (1.0f / 16777216.0f);
   const float u2 = u24(b);
-  const float r = sqrtf(__fmul_rn(-2.0f, logf(u1)));
-  const float th = __fmul_rn(6.2831854820251465f, u2);
+  const float r = sqrtf(-2.0f * logf(u1));
+  const float th = 6.2831854820251465f * u2;
   float s, c;
   sincosf(th, &s, &c);
-  z0 = __fmul_rn(r, c);
-  z1 = __fmul_rn(r, s);
+  z0 = r * c;
+  z1 = r * s;
 }
 
 template <typename T, typename Op>
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(GT) void generate_kernel(uint64_t seed, uint64_t fi
   }
   mn = block_reduce(mn, s_redf, [](float a, float b) { return fminf(a, b); });
   mx = block_reduce(mx, s_redf, [](float a, float b) { return fmaxf(a, b); });
-  const float den = __fadd_rn(mx - mn, 1e-8f);
+  const float den = (mx - mn) + 1e-8f;
 
   // ---- phase B: signal power of the normalised signal (数据集产生.py:38-43) --------------------
   double ps = 0.0;
@@ -141,7 +144,7 @@ __global__ __launch_bounds__(GT) void generate_kernel(uint64_t seed, uint64_t fi
       int width = randint(20, 100, sp.x), start = 0;
       if (L - width <= 0) width = L;               // the reference would raise here
       else start = randint(0, L - width, sp.y);
-      const float amp = __fmul_rn(uniform(5.0f, 15.0f, sp.z), sigma);
+      const float amp = uniform(5.0f, 15.0f, sp.z) * sigma;
       s_spk[s][0] = (float)start;
       s_spk[s][1] = (float)width;
       s_spk[s][2] = u24(sp.w) > 0.5f ? amp : -amp;
@@ -166,10 +169,10 @@ __global__ __launch_bounds__(GT) void generate_kernel(uint64_t seed, uint64_t fi
       const int p = p0 + i;
       if (p >= L) break;
       const float c = __fdiv_rn(cl[p] - mn, den);
-      float v = __fadd_rn(c, __fmul_rn(sigma, z[i]));
+      float v = c + sigma * z[i];
       for (int s = 0; s < ns; ++s) {
         const int st = (int)s_spk[s][0], w = (int)s_spk[s][1];
-        if (p >= st && p < st + w) v = __fadd_rn(v, s_spk[s][2]);
+        if (p >= st && p < st + w) v = v + s_spk[s][2];
       }
       cl[p] = c;
       nz[p] = v;

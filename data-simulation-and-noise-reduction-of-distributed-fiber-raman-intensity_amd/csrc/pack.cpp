@@ -121,6 +121,7 @@ std::vector<std::string> param_names(const std::vector<Op>& spec) {
   return out;
 }
 
+// bf16 keeps the head as an MFMA layer (M-row 0); f32 and bf16x3 run the head on the VALU
 int big_layers(const std::vector<Op>& spec, int dtype) {
   int n = 0;
   for (const Op& o : spec) n += o.kind == OpKind::BIG || (o.kind == OpKind::HEAD && dtype == BF16);
@@ -211,6 +212,27 @@ static void pack_big_f32(const Folded& f, uint8_t* dst) {
   for (int c = 0; c < C; ++c) bias[c] = (float)f.b[c];
 }
 
+static void pack_big_x3(const Folded& f, uint8_t* dst) {
+  uint16_t* frag = (uint16_t*)dst;
+  for (int m = 0; m < 4; ++m)
+    for (int s = 0; s < 6; ++s)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int t = s >> 1, u = s & 1;
+          const int co = 16 * m + (lane & 15), ci = 32 * u + 8 * (lane >> 4) + j;
+          const float w = (float)f.W(co, ci, t);
+          const uint16_t hi = to_bf16(w);
+          const uint32_t hib = (uint32_t)hi << 16;
+          float hf;
+          std::memcpy(&hf, &hib, 4);
+          const uint16_t lo = to_bf16((double)w - (double)hf);
+          frag[((((m * 6 + s) * 2 + 0) * 64) + lane) * 8 + j] = hi;
+          frag[((((m * 6 + s) * 2 + 1) * 64) + lane) * 8 + j] = lo;
+        }
+  float* bias = (float*)(dst + BIG_FRAG_FLOATS_F32 * 4);
+  for (int c = 0; c < C; ++c) bias[c] = (float)f.b[c];
+}
+
 static void pack_small_conv(const Folded& f, float* slot) {   // w[c*3+t], bias at 192 (+c)
   std::memset(slot, 0, SMALL_SLOT_FLOATS * sizeof(float));
   if (f.cin == 1) {
@@ -259,12 +281,13 @@ size_t packed_bytes(const std::vector<Op>& spec, int dtype) {
   return SMALL_BYTES + (size_t)big_layers(spec, dtype) * (dtype == BF16 ? BIG_BYTES_BF16 : BIG_BYTES_F32);
 }
 
+
 // returns "" on success, else the error message
 std::string pack(int arch, int dtype, const float* const* tensors, const int64_t* numels, int n, void* dst,
                  size_t cap) {
   const std::vector<Op> spec = net_spec(arch);
   if (spec.empty()) return "unknown arch " + std::to_string(arch);
-  if (dtype != F32 && dtype != BF16) return "unknown dtype " + std::to_string(dtype);
+  if (dtype != F32 && dtype != BF16 && dtype != BF16X3) return "unknown dtype " + std::to_string(dtype);
   const size_t need = packed_bytes(spec, dtype);
   if (cap < need) return "destination too small: need " + std::to_string(need) + " bytes";
   uint8_t* out = (uint8_t*)dst;
@@ -284,6 +307,7 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
       case OpKind::BIG:
         if (!fold(rd, o, C, C, f)) return rd.err;
         if (dtype == BF16) pack_big_bf16(f, big + layer * big_bytes);
+        else if (dtype == BF16X3) pack_big_x3(f, big + layer * big_bytes);
         else pack_big_f32(f, big + layer * big_bytes);
         ++layer;
         break;

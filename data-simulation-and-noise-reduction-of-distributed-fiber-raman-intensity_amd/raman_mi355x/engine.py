@@ -12,7 +12,7 @@ from . import _lib
 
 ARCHS = ("DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN")
 ARCH_ID = {a: i for i, a in enumerate(ARCHS)}
-DTYPE_ID = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}
+DTYPE_ID = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "bf16x3": 2}
 
 
 def _arch(arch):

@@ -45,9 +45,10 @@ class _EngineNet(nn.Module):
         return self._engine_dtype
 
     def set_engine_dtype(self, dtype):
-        """'fp32' (exact-fp32 MFMA; 1e-5 parity) or 'bf16' (bf16 MFMA, fp32 accumulate)."""
-        engine._dtype(dtype)
-        self._engine_dtype = "bf16" if dtype in ("bf16", "bfloat16", torch.bfloat16) else "fp32"
+        """'fp32' (exact-fp32 MFMA, 1e-5 parity), 'bf16' (one bf16 MFMA per product, fastest) or
+        'bf16x3' (split-bf16, three bf16 MFMAs per product: bf16 speed class, ~1e-4 accuracy)."""
+        code = engine._dtype(dtype)
+        self._engine_dtype = {0: "fp32", 1: "bf16", 2: "bf16x3"}[code]
         return self
 
     # -- packing -----------------------------------------------------------------------------

@@ -44,7 +44,12 @@ typedef enum {
   RDN_APIDN = 5       /* APIDN/train.py   class APIDN      */
 } rdn_arch;
 
-typedef enum { RDN_F32 = 0, RDN_BF16 = 1 } rdn_dtype;
+/* Arithmetic of the 64->64 convolutions (stems, heads, bias, activations math: fp32 always).
+ *   RDN_F32    exact-fp32 MFMA, fp32 activations               (1e-5 parity mode)
+ *   RDN_BF16   one bf16 MFMA per product, bf16 activations      (fastest)
+ *   RDN_BF16X3 split bf16: operands as bf16 hi+lo pairs, three bf16 MFMAs per product
+ *              (hi*hi + hi*lo + lo*hi), ~16-bit operands        (bf16 MFMA at 2e-2-safe accuracy) */
+typedef enum { RDN_F32 = 0, RDN_BF16 = 1, RDN_BF16X3 = 2 } rdn_dtype;
 
 enum {
   RDN_OK = 0,

@@ -1,11 +1,14 @@
+# GPU round check: parity tests, then short benches for each engine dtype, then a kernel-trace profile.
 set +e
-cd /root/repo
+cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 240 python -u bench.py --steps 10 --warmup 2 --cpu-seconds 5 > gpurun_out/bench.log 2>&1
-rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
-if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o r1 -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1
-echo "prof rc=$?"
+for dt in bf16 bf16x3 fp32; do
+  B=8192; [ $dt = fp32 ] && B=1024; [ $dt = bf16x3 ] && B=2048
+  timeout -k 10 200 python -u bench.py --dtype $dt --batch $B --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/bench_$dt.log 2>&1
+  rc=$?; echo "bench $dt rc=$rc"; tail -1 gpurun_out/bench_$dt.log | cut -c1-400
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done

@@ -11,7 +11,8 @@ classes and ``generate_signals`` without executing the training / dataset script
 * ``model_<Arch>.npz``      — per network: state_dict key list/shapes (the drop-in contract),
                               reference fp32 CPU outputs on ``inputs.npz`` for synthetic weights
                               (``oracle.weights.synth_state_dict(seed=1234)``), and for the briefly
-                              trained networks (RRCDNet, DenoiseCNN, PIDN) also the trained weights and outputs.
+                              trained networks (RRCDNet, DenoiseCNN, PIDN) also the trained weights and outputs;
+                              ``f64_*``: the same reference modules run in float64 (exact forward).
 * ``metrics.npz``           — per-spectrum MSE/SSIM/Smoothness/Peak2Peak computed by the reference
                               metric functions (*/evaulate.py:14-21) and scikit-image 0.18.3
                               (``/opt/conda/bin/python3.9``) on (clean, denoised) pairs.
@@ -95,12 +96,26 @@ def train_briefly(cls, gen, steps=300, L=1000, batch=8, lr=1e-3):
 
 
 @torch.no_grad()
-def ref_outputs(cls, sd, sets):
+def ref_outputs(cls, sd, sets, double=False):
+    """Reference forward; double=True runs the same reference module in float64 (the 'exact'
+    forward used to judge fp32 results when the fp32 reference's own rounding is the floor)."""
     m = cls()
     m.load_state_dict(sd, strict=True)
     m.eval()
-    return {name: m(torch.from_numpy(x).unsqueeze(1)).squeeze(1).numpy().astype(np.float32)
-            for name, x in sets.items()}
+    if double:
+        m = m.double()
+    return {name: m(torch.from_numpy(x).unsqueeze(1).to(torch.float64 if double else torch.float32))
+            .squeeze(1).numpy().astype(np.float32) for name, x in sets.items()}
+
+
+def previous_trained(arch):
+    """Reuse the committed trained weights (CPU training is not bit-reproducible across machines)."""
+    path = os.path.join(HERE, f"model_{arch}.npz")
+    if not os.path.exists(path) or "--retrain" in sys.argv:
+        return None
+    g = np.load(path)
+    keys = [k[3:] for k in g.files if k.startswith("w::")]
+    return {k: torch.from_numpy(np.array(g["w::" + k])) for k in keys} if keys else None
 
 
 def gen_stats(gen):
@@ -181,13 +196,17 @@ def main():
         rec["synth_gain"] = np.array(GAIN[arch])
         for name, y in ref_outputs(cls, sd, sets).items():
             rec[f"synth_{name}"] = y
+        for name, y in ref_outputs(cls, sd, sets, double=True).items():
+            rec[f"f64_synth_{name}"] = y
         if arch in TRAINED:
-            tsd = train_briefly(cls, gen)
+            tsd = previous_trained(arch) or train_briefly(cls, gen)
             for k, v in tsd.items():
                 rec[f"w::{k}"] = v.numpy()
             outs = ref_outputs(cls, tsd, sets)
             for name, y in outs.items():
                 rec[f"trained_{name}"] = y
+            for name, y in ref_outputs(cls, tsd, sets, double=True).items():
+                rec[f"f64_trained_{name}"] = y
             trained_outputs[arch] = outs["main"]
         np.savez_compressed(os.path.join(HERE, f"model_{arch}.npz"), **rec)
         print(f"{arch}: {len(keys)} keys; out range main "

@@ -1,0 +1,149 @@
+"""C-ABI checks that need no GPU: the library loads, exports every declared entry point, names the
+reference state_dict keys, and packs (BN folding + MFMA fragment layout) exactly as documented."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, golden_state_dict
+
+ARCHS = ["DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN"]
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from raman_mi355x import _lib
+    return _lib.lib()
+
+
+def test_exports_every_declared_symbol(lib):
+    with open(os.path.join(ROOT, "include", "raman_mi355x.h")) as fh:
+        header = fh.read()
+    declared = set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+(rdn_\w+)\s*\(", header, re.M))
+    from raman_mi355x import _lib
+    assert declared == set(_lib.EXPORTED), declared ^ set(_lib.EXPORTED)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.rdn_version() == 1
+
+
+@pytest.mark.parametrize("arch", ARCHS)
+def test_param_names_are_reference_keys(arch):
+    from raman_mi355x import engine
+    from conftest import load_golden
+    import json
+    keys = json.loads(str(load_golden(arch)["keys"]))
+    names = engine.param_names(arch)
+    assert len(names) == len(set(names))
+    assert set(names) <= set(keys)
+    # everything except the BN step counters feeds the engine
+    assert set(keys) - set(names) == {k for k in keys if k.endswith("num_batches_tracked")}
+    # order follows the state_dict order (the forward order of the reference modules)
+    assert names == [k for k in keys if k in set(names)]
+
+
+def test_errors_are_reported_not_raised(lib):
+    from raman_mi355x import engine, _lib
+    n = ctypes.c_size_t()
+    assert lib.rdn_packed_size(99, 0, ctypes.byref(n)) == -1
+    assert b"bad argument" in lib.rdn_last_error()
+    sd = golden_state_dict("DenoiseCNN", "synth")
+    sd["layers.2.0.weight"] = sd["layers.2.0.weight"][:, :32]        # wrong shape
+    with pytest.raises(_lib.EngineError, match="expected 12288 elements"):
+        engine.pack("DenoiseCNN", sd, "fp32", "cpu")
+    with pytest.raises(KeyError):
+        engine.pack("DenoiseCNN", {}, "fp32", "cpu")
+
+
+def _fold(sd, conv, bn):
+    w = sd[conv + ".weight"].double().numpy()
+    b = sd[conv + ".bias"].double().numpy()
+    if bn:
+        s = sd[bn + ".weight"].double().numpy() / np.sqrt(sd[bn + ".running_var"].double().numpy() + 1e-5)
+        w = w * s[:, None, None]
+        b = (b - sd[bn + ".running_mean"].double().numpy()) * s + sd[bn + ".bias"].double().numpy()
+    return w.astype(np.float32), b.astype(np.float32)
+
+
+def _bf16_to_f32(u16):
+    return (u16.astype(np.uint32) << 16).view(np.float32)
+
+
+def _f32_to_bf16(f):
+    u = f.astype(np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+SMALL = 64 * 256 * 4
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3"])
+def test_pack_layout_rrcdnet(dtype):
+    """Unpack the blob with the layout documented in csrc/common.hpp and compare with BN folding."""
+    from raman_mi355x import engine
+    sd = golden_state_dict("RRCDNet", "trained")
+    blob = engine.pack("RRCDNet", sd, dtype, "cpu").numpy()
+    assert blob.size == engine.packed_size("RRCDNet", dtype)
+    small = blob[:SMALL].view(np.float32).reshape(64, 256)
+    # stem of the right branch: slot 0, BN folded
+    w, b = _fold(sd, "right_net.0", "right_net.1")
+    np.testing.assert_allclose(small[0, :192].reshape(64, 3), w[:, 0, :], rtol=1e-6)
+    np.testing.assert_allclose(small[0, 192:], b, rtol=1e-6, atol=1e-7)
+    # left head: slot 3
+    w, b = _fold(sd, "left_net.19", None)
+    np.testing.assert_array_equal(small[3, :192].reshape(64, 3), w[0])
+    assert small[3, 192] == b[0]
+    # big layer 16 = left_net.3.0 (first dilated conv) in every dtype's order
+    big = blob[SMALL:]
+    if dtype == "bf16":
+        layer, nbytes = 16, 24832              # the right head is big layer 15 in bf16
+    else:
+        layer, nbytes = 15, 49408
+    w, b = _fold(sd, "left_net.3.0", None)
+    L = big[layer * nbytes:(layer + 1) * nbytes]
+    lane = np.arange(64)
+    if dtype == "fp32":
+        frag = L[:49152].view(np.float32).reshape(4, 12, 64, 4)
+        for m in range(4):
+            for tg in range(12):
+                t, g = tg >> 2, tg & 3
+                for i in range(4):
+                    exp = w[16 * m + (lane & 15), 16 * g + 4 * (lane >> 4) + i, t]
+                    np.testing.assert_array_equal(frag[m, tg, :, i], exp)
+        np.testing.assert_array_equal(L[49152:49408].view(np.float32), b)
+    elif dtype == "bf16":
+        frag = L[:24576].view(np.uint16).reshape(4, 6, 64, 8)
+        for m in range(4):
+            for s in range(6):
+                t, u = s >> 1, s & 1
+                for j in range(8):
+                    exp = w[16 * m + (lane & 15), 32 * u + 8 * (lane >> 4) + j, t]
+                    np.testing.assert_array_equal(frag[m, s, :, j], _f32_to_bf16(exp))
+        np.testing.assert_array_equal(L[24576:24832].view(np.float32), b)
+    else:
+        frag = L[:49152].view(np.uint16).reshape(4, 6, 2, 64, 8)
+        for m in range(4):
+            for s in range(6):
+                t, u = s >> 1, s & 1
+                for j in range(8):
+                    exp = w[16 * m + (lane & 15), 32 * u + 8 * (lane >> 4) + j, t]
+                    hi = _bf16_to_f32(frag[m, s, 0, :, j])
+                    lo = _bf16_to_f32(frag[m, s, 1, :, j])
+                    np.testing.assert_array_equal(frag[m, s, 0, :, j], _f32_to_bf16(exp))
+                    assert np.all(np.abs(hi.astype(np.float64) + lo - exp) <= 2.0 ** -16 * np.abs(exp) + 1e-30)
+        np.testing.assert_array_equal(L[49152:49408].view(np.float32), b)
+
+
+def test_bn_folding_matches_reference_math():
+    """Folding is exact in fp64: conv(x, W') + b' == BN(conv(x, W) + b) to fp32 rounding."""
+    sd = golden_state_dict("RRCDNet", "trained")
+    x = torch.randn(2, 64, 300, dtype=torch.float64)
+    w, b = _fold(sd, "right_net.5.0", "right_net.5.1")
+    y_fold = torch.nn.functional.conv1d(x, torch.from_numpy(w).double(), torch.from_numpy(b).double(), padding=1)
+    y = torch.nn.functional.conv1d(x, sd["right_net.5.0.weight"].double(), sd["right_net.5.0.bias"].double(), padding=1)
+    y = torch.nn.functional.batch_norm(y, sd["right_net.5.1.running_mean"].double(), sd["right_net.5.1.running_var"].double(),
+                                       sd["right_net.5.1.weight"].double(), sd["right_net.5.1.bias"].double(), False, 0, 1e-5)
+    assert (y_fold - y).abs().max() / y.abs().max() < 1e-6

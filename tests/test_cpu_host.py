@@ -1,0 +1,153 @@
+"""Host-side checks without a GPU: oracle vs the reference's golden vectors, module surfaces,
+dataset format, sharding, and the world_size-2 metric all-reduce over gloo."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN, INPUT_SETS, golden_inputs, golden_state_dict, golden_template, input_array, load_golden
+
+ARCHS = ["DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN"]
+
+
+# --- oracle pinned to the reference ------------------------------------------------------------
+@pytest.mark.parametrize("arch", ARCHS)
+def test_oracle_reproduces_reference_outputs(arch, inputs):
+    from oracle.models import forward
+    g = load_golden(arch)
+    whichs = ["synth"] + (["trained"] if any(k.startswith("w::") for k in g.files) else [])
+    sets = ["main", "edge7", "edge33"] if arch in ("ADSDN", "APIDN") else INPUT_SETS
+    for which in whichs:
+        sd = golden_state_dict(arch, which)
+        for name in sets:
+            x = torch.from_numpy(input_array(inputs, name)).unsqueeze(1)
+            y = forward(arch, sd, x).squeeze(1).numpy()
+            ref = g[f"{which}_{name}"]
+            assert np.abs(y - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max()), (arch, which, name)
+
+
+def test_oracle_metrics_match_skimage_golden():
+    from oracle.metrics import per_spectrum
+    g = np.load(os.path.join(GOLDEN, "metrics.npz"))
+    p = per_spectrum(g["den"], g["clean"])
+    ref = g["per_spectrum"]
+    np.testing.assert_allclose(p[:, :2], ref[:, :2], rtol=1e-10)      # MSE, SSIM (fp64 in both)
+    np.testing.assert_allclose(p[:, 2:], ref[:, 2:], rtol=1e-6)       # reference: float32 diff/ptp
+
+
+def test_oracle_generator_distribution():
+    """The numpy restatement of the engine's simulator against reference statistics (small n)."""
+    from oracle.generator import generate
+    with open(os.path.join(GOLDEN, "generator_stats.json")) as fh:
+        ref = json.load(fh)
+    c, x, s, sd, outs = generate(7, 0, 200, 10000)
+    assert np.all(c.min(axis=1) == 0) and np.all(c.max(axis=1) > 0.9999)
+    lens = np.concatenate([o["seg_lens"][:-1] for o in outs])
+    assert lens.min() >= 1 and lens.max() <= 40 and abs(lens.mean() - 20.5) < 0.5
+    assert s.min() >= 20 and s.max() < 37
+    assert abs(np.mean(np.mean(c.astype(np.float64) ** 2, axis=1)) - ref["power_mean"]) < 0.02
+    rq = np.array(ref["noise_std_quantiles"])
+    assert rq[0] * 0.8 < np.median(sd) < rq[4]
+
+
+def test_oracle_generator_is_counter_based():
+    from oracle.generator import generate_one
+    a = generate_one(11, 5, 500)
+    b = generate_one(11, 5, 500)
+    c = generate_one(11, 6, 500)
+    assert np.array_equal(a["noisy"], b["noisy"]) and not np.array_equal(a["noisy"], c["noisy"])
+
+
+# --- module surface ----------------------------------------------------------------------------
+@pytest.mark.parametrize("arch", ARCHS)
+def test_module_state_dict_is_reference_compatible(arch):
+    import raman_mi355x as R
+    g = load_golden(arch)
+    m = R.MODELS[arch]()
+    keys = json.loads(str(g["keys"]))
+    shapes = json.loads(str(g["shapes"]))
+    sd = m.state_dict()
+    assert list(sd) == keys
+    assert [list(v.shape) for v in sd.values()] == shapes
+    m.load_state_dict(golden_state_dict(arch, "synth"), strict=True)
+
+
+def test_module_refuses_cpu_and_training():
+    import raman_mi355x as R
+    m = R.PIDN()
+    with pytest.raises(RuntimeError, match="inference-only"):
+        m.train()(torch.zeros(1, 1, 16))
+    with pytest.raises(RuntimeError, match="GPU only"):
+        m.eval()(torch.zeros(1, 1, 16))
+    with pytest.raises(NotImplementedError):
+        R.DSDN(num_res_blocks=3)
+
+
+def test_checkpoint_round_trip(tmp_path):
+    """torch.save(state_dict) -> torch.load(weights_only=True) -> strict load, as */evaulate.py:66."""
+    import raman_mi355x as R
+    sd = golden_state_dict("RRCDNet", "trained")
+    path = tmp_path / "RRCDNet_best.pth"
+    torch.save(sd, path)
+    m = R.RRCDNet()
+    m.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, sd[k])
+
+
+def test_dataset_format(tmp_path):
+    from raman_mi355x.dataset import load_dataset, save_dataset
+    rng = np.random.default_rng(0)
+    c, n = rng.uniform(size=(3, 50)), rng.uniform(size=(3, 50))
+    save_dataset(tmp_path / "test.npz", c, n, np.ones(3), np.ones(3) * 0.1)
+    d = load_dataset(tmp_path / "test.npz")
+    assert d["clean_signals"].dtype == np.float64 and d["snrs"].shape == (3, 1)
+    np.testing.assert_array_equal(d["noisy_signals"], n)
+
+
+# --- data parallelism --------------------------------------------------------------------------
+def test_shard_partitions_exactly():
+    from raman_mi355x.distributed import shard
+    for n in (0, 1, 7, 1000, 1001):
+        for w in (1, 2, 3, 8):
+            parts = [shard(n, r, w) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+            assert max(b - a for a, b in parts) - min(b - a for a, b in parts) <= 1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _allreduce_worker(rank, world, port, per, out):
+    import torch.distributed as dist
+    from raman_mi355x.distributed import all_reduce_sums, means, shard
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    lo, hi = shard(per.shape[0])
+    sums = torch.cat([torch.from_numpy(per[lo:hi]).sum(0), torch.tensor([float(hi - lo)], dtype=torch.float64)])
+    all_reduce_sums(sums)
+    if rank == 0:
+        out.update(means(sums))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_metric_allreduce_world2_gloo():
+    """Rank-sharded metric sums all-reduced over gloo equal the single-process means."""
+    g = np.load(os.path.join(GOLDEN, "metrics.npz"))
+    per = g["per_spectrum"].astype(np.float64)
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_allreduce_worker, args=(2, port, per, out), nprocs=2, join=True)
+        got = dict(out)
+    exp = per.mean(axis=0)
+    for i, k in enumerate(("MSE", "SSIM", "Smoothness", "Peak2Peak")):
+        assert abs(got[k] - exp[i]) <= 1e-12 * max(1.0, abs(exp[i]))
