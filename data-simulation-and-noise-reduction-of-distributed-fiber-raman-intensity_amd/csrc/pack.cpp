@@ -121,10 +121,23 @@ std::vector<std::string> param_names(const std::vector<Op>& spec) {
   return out;
 }
 
-// bf16 keeps the head as an MFMA layer (M-row 0); f32 and bf16x3 run the head on the VALU
+// Weight layout of the big section: the fused bf16 kernels (non-CBAM networks, bf16) keep the
+// head as an MFMA layer (M-row 0) in 24832-byte layers; every other (network, dtype) runs on the
+// in-place 256-byte-row engine: f32 fragments, or bf16 hi/lo fragments (bf16 uses only hi).
+static bool has_cbam(const std::vector<Op>& spec) {
+  for (const Op& o : spec)
+    if (o.kind == OpKind::CBAM) return true;
+  return false;
+}
+int big_layout(const std::vector<Op>& spec, int dtype) {
+  if (dtype == F32) return F32;
+  if (dtype == BF16 && !has_cbam(spec)) return BF16;
+  return BF16X3;
+}
 int big_layers(const std::vector<Op>& spec, int dtype) {
+  const bool head_big = big_layout(spec, dtype) == BF16;
   int n = 0;
-  for (const Op& o : spec) n += o.kind == OpKind::BIG || (o.kind == OpKind::HEAD && dtype == BF16);
+  for (const Op& o : spec) n += o.kind == OpKind::BIG || (o.kind == OpKind::HEAD && head_big);
   return n;
 }
 
@@ -278,7 +291,7 @@ static bool pack_cbam(Reader& rd, const Op& o, float* small) {
 }
 
 size_t packed_bytes(const std::vector<Op>& spec, int dtype) {
-  return SMALL_BYTES + (size_t)big_layers(spec, dtype) * (dtype == BF16 ? BIG_BYTES_BF16 : BIG_BYTES_F32);
+  return SMALL_BYTES + (size_t)big_layers(spec, dtype) * (big_layout(spec, dtype) == BF16 ? BIG_BYTES_BF16 : BIG_BYTES_F32);
 }
 
 
@@ -294,7 +307,8 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
   std::memset(out, 0, need);
   float* small = (float*)out;
   uint8_t* big = out + SMALL_BYTES;
-  const size_t big_bytes = dtype == BF16 ? BIG_BYTES_BF16 : BIG_BYTES_F32;
+  const int layout = big_layout(spec, dtype);
+  const size_t big_bytes = layout == BF16 ? BIG_BYTES_BF16 : BIG_BYTES_F32;
   Reader rd{tensors, numels, n};
   int layer = 0;
   for (const Op& o : spec) {
@@ -306,15 +320,15 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
         break;
       case OpKind::BIG:
         if (!fold(rd, o, C, C, f)) return rd.err;
-        if (dtype == BF16) pack_big_bf16(f, big + layer * big_bytes);
-        else if (dtype == BF16X3) pack_big_x3(f, big + layer * big_bytes);
+        if (layout == BF16) pack_big_bf16(f, big + layer * big_bytes);
+        else if (layout == BF16X3) pack_big_x3(f, big + layer * big_bytes);
         else pack_big_f32(f, big + layer * big_bytes);
         ++layer;
         break;
       case OpKind::HEAD:
         if (!fold(rd, o, C, 1, f)) return rd.err;
         pack_small_conv(f, small + o.slot * SMALL_SLOT_FLOATS);
-        if (dtype == BF16) pack_big_bf16(f, big + (layer++) * big_bytes);
+        if (layout == BF16) pack_big_bf16(f, big + (layer++) * big_bytes);
         break;
       case OpKind::CBAM:
         if (!pack_cbam(rd, o, small)) return rd.err;

@@ -21,7 +21,7 @@ from conftest import INPUT_SETS, golden_state_dict, input_array, load_golden
 
 pytestmark = pytest.mark.gpu
 
-FUSED = ["DenoiseCNN", "RRCDNet", "DSDN", "PIDN"]
+FUSED = ["DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN"]
 TRAINED = ["DenoiseCNN", "RRCDNet", "PIDN"]
 F32_REL = 1e-5
 BF16_ABS = 2e-2
