@@ -1,6 +1,10 @@
 """Headline benchmark: denoised spectra/s of the fused RRCDNet forward on MI355X (BASELINE.json).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--arch RRCDNet] [--dtype bf16] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--arch RRCDNet] [--dtype bf16x3] [--batch B]
+
+The headline dtype is bf16x3: bf16 MFMA arithmetic with split (hi + lo) operands, the engine's bf16
+mode that meets the north-star bf16 tolerance (2e-2 max-abs) on trained weights.  Plain single-
+rounding bf16 and exact fp32 are timed as "variants" in the same line.
 
 One step = one forward of the fused network over a batch of B synthetic spectra per GPU (L = 10000),
 generated on-device by the engine's simulator BEFORE the timed region (inputs resident in HBM).
@@ -59,18 +63,44 @@ def cpu_baseline(arch, L, seconds):
                       f"{torch.get_num_threads()} threads, loop shape of evaulate.py:29-32)"}
 
 
+def traffic_per_spectrum(arch, dtype):
+    """HBM bytes per spectrum of the dominant kernel from the committed rocprofv3 PMC summary
+    (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md §HBM), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as fh:
+            rec = json.load(fh).get(f"{arch}/{dtype}")
+        return (rec["bytes_per_spectrum"], rec["source"]) if rec else (None, None)
+    except (OSError, ValueError, KeyError):
+        return None, None
+
+
+def time_forward(engine, arch, dtype, packed, x, y, steps, warmup, stream):
+    for _ in range(warmup):
+        engine.forward(arch, dtype, packed, x, out=y)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        engine.forward(arch, dtype, packed, x, out=y)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--arch", default="RRCDNet")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "bf16x3", "fp32"])
+    ap.add_argument("--dtype", default="bf16x3", choices=["bf16", "bf16x3", "fp32"])
     ap.add_argument("--batch", type=int, default=8192, help="spectra per GPU per step")
     ap.add_argument("--L", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=20250410)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-variants", action="store_true", help="skip timing the other engine dtypes")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,11 +156,24 @@ def main():
         dist.all_reduce(sums)
     sums = sums.cpu().tolist()
 
+    variants = {}
+    if not args.no_variants:
+        for dt in ("bf16x3", "bf16", "fp32"):
+            if dt == args.dtype:
+                continue
+            nb = B if dt != "fp32" else max(1, B // 4)
+            pk = model.set_engine_dtype(dt).packed_weights(dev)
+            ms = time_forward(engine, args.arch, dt, pk, x[:nb], y[:nb], 3, 1, stream)
+            variants[dt] = {"spectra_per_s_per_gpu": nb / (ms * 1e-3), "kernel_ms": ms, "batch": nb,
+                            "roofline_frac": flops_per_spectrum(args.arch, L) * nb / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[dt]}
+        model.set_engine_dtype(args.dtype)
+
     if rank == 0:
         total = world * B * args.steps
         fl = flops_per_spectrum(args.arch, L) * B              # per launch
         achieved = fl / (kernel_ms * 1e-3) / 1e12
         peak = PEAK_TFLOPS[args.dtype]
+        tps, tsrc = traffic_per_spectrum(args.arch, args.dtype)
         rec = {
             "metric": METRIC, "value": total / elapsed, "unit": "spectra/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
@@ -141,8 +184,11 @@ def main():
                        "arch": args.arch, "signal_length": L, "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": None,
-                         "kernel_ms": kernel_ms, "flops_per_launch": fl},
+                         "frac": achieved / peak, "traffic": tps * B if tps else None,
+                         "traffic_source": tsrc, "algorithmic_bytes": 8 * L * B,
+                         "kernel_ms": kernel_ms, "flops_per_launch": fl,
+                         "mfma_products_per_flop": 3 if args.dtype == "bf16x3" else 1},
+            "variants": variants,
             "metrics_mean": {k: sums[i] / sums[4] for i, k in enumerate(["MSE", "SSIM", "Smoothness", "Peak2Peak"])},
         }
         if world == 1 and not args.no_cpu_baseline:

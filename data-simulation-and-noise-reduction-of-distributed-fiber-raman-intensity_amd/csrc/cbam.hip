@@ -235,13 +235,16 @@ __global__ __launch_bounds__(THREADS) void segment(const uint8_t* __restrict__ b
   Tile tl = make_tile(lds, blob, x, L, T, tiles, sg.halo, n);
   tl.layer = sg.layer0;
   f32x4 id[16];
+  typename Op<MODE>::A a;
+  if (sg.n_convs) a = load_a0<MODE>(tl, sg.layer0);
   zero_guards(lds);
   if (sg.pro == PRO_STEM) prologue_stem<MODE>(tl, sg, n);
   else prologue_cbam<MODE>(tl, sg, n);
   __syncthreads();
   for (int i = 0; i < sg.n_convs; ++i) {
-    if ((i ? sg.epi1 : sg.epi0) & RELU) conv<MODE, RELU, G::NG, G::S>(tl, 1, id);
-    else conv<MODE, 0, G::NG, G::S>(tl, 1, id);
+    const bool more = i + 1 < sg.n_convs;
+    if ((i ? sg.epi1 : sg.epi0) & RELU) conv<MODE, RELU, G::S>(tl, 1, id, a, more);
+    else conv<MODE, 0, G::S>(tl, 1, id, a, more);
   }
   if (sg.epi == EPI_STORE) {
     epilogue_store<MODE>(tl, sg, n);

@@ -48,15 +48,22 @@ constexpr int BIG_BYTES_F32 = (BIG_FRAG_FLOATS_F32 + C) * 4;               // 49
 // ds_read_b128 B-fragment reads for any row offset, 2-way ds_write_b64 epilogue stores.
 constexpr int ROWB_BF16 = C * 2;
 constexpr int ACT_BYTES_BF16 = ROWS * ROWB_BF16;                           // 66048
-// f32 activation buffer: ROWS x 256 B, slots swizzled by 2*(row & 7).
+// f32 / split-bf16 activation buffer: ROWS x 256 B, slots swizzled by swz256(row).
 constexpr int ROWB_F32 = C * 4;
 constexpr int ACT_BYTES_F32 = ROWS * ROWB_F32;                             // 132096
 
 __device__ __forceinline__ uint32_t off_bf16(int prow, int byte) {
   return (uint32_t)(prow * ROWB_BF16) + ((((byte >> 4) ^ (prow & 7)) << 4) | (byte & 15));
 }
+// 256-byte rows: 16-B slot s of row r lives at slot s ^ f(r), f linear over the low 3 row bits
+// (masks 2, 7, 14; found by exhaustive search with the lane-group bank model of
+// MI355X_MICROARCH.md §LDS): conflict-free ds_read_b128 B fragments (f32 and split-bf16) and
+// ds_write_b128 f32 stores, 2-way ds_write_b64 split-bf16 stores (the floor at 16-B granularity).
+__device__ __forceinline__ int swz256(int prow) {
+  return ((prow & 1) ? 2 : 0) ^ ((prow & 2) ? 7 : 0) ^ ((prow & 4) ? 14 : 0);
+}
 __device__ __forceinline__ uint32_t off_f32(int prow, int byte) {
-  return (uint32_t)(prow * ROWB_F32) + ((((byte >> 4) ^ ((prow & 7) << 1)) << 4) | (byte & 15));
+  return (uint32_t)(prow * ROWB_F32) + ((((byte >> 4) ^ swz256(prow)) << 4) | (byte & 15));
 }
 
 enum Arch : int { DENOISECNN = 0, RRCDNET = 1, DSDN = 2, ADSDN = 3, PIDN = 4, APIDN = 5 };

@@ -113,6 +113,8 @@ __device__ __forceinline__ void conv(Tile& tl, uint32_t src, uint32_t dst, int d
   const char* wslot = tl.lds + WSLOT;
   bf16x8 A[4][6];
   f32x4 bias[4];
+  const int r0 = tl.base + w * 64;                  // this wave's 64 rows straddle no spectrum end?
+  const bool wave_inside = r0 >= 0 && r0 + 64 <= tl.L;
 
 #pragma unroll
   for (int n = 0; n < 4; ++n) {
@@ -137,28 +139,16 @@ __device__ __forceinline__ void conv(Tile& tl, uint32_t src, uint32_t dst, int d
       for (int m = 0; m < 4; ++m)
         bias[m] = *(const f32x4*)(wslot + BIG_FRAG_BYTES_BF16 + (16 * m + 4 * q) * 4);
     }
-    // ---- epilogue for this N-tile ----
-    const int p = tl.base + row;
-    const bool valid = in_range(p, tl.L);
+    // ---- epilogue for this N-tile: bias (+ identity), ReLU, zero rows outside [0, L) ----
+    const bool valid = wave_inside || in_range(tl.base + row, tl.L);
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const uint32_t o = dst + off_bf16(row + GUARD, 32 * m + 8 * q);
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[m][r] + bias[m][r];
-      if (EPI == EPI_RES_RELU) {
-        const bf16x4 id = *(const bf16x4*)(tl.lds + o);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += (float)id[r];
-      }
-      bf16x4 out;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float a = v[r];
-        if (EPI == EPI_RELU || EPI == EPI_RES_RELU) a = fmaxf(a, 0.f);
-        out[r] = (__bf16)(valid ? a : 0.f);
-      }
-      *(bf16x4*)(tl.lds + o) = out;
+      f32x4 v = acc[m] + bias[m];
+      if (EPI == EPI_RES_RELU) v += __builtin_convertvector(*(const bf16x4*)(tl.lds + o), f32x4);
+      if (EPI == EPI_RELU || EPI == EPI_RES_RELU) v = __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
+      if (!valid) v = f32x4{0.f, 0.f, 0.f, 0.f};
+      *(bf16x4*)(tl.lds + o) = __builtin_convertvector(v, bf16x4);
     }
     if (n == 0) {
       // every wave now holds this layer's A-fragments and bias in VGPRs: refill the slot

@@ -20,10 +20,11 @@ IP_KERNEL(denoisecnn) {
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, H, n);
   f32x4 id[16];
+  typename Op<MODE>::A a = load_a0<MODE>(tl, 0);
   zero_guards(lds);
   stem<MODE>(tl, 0);
   __syncthreads();
-  for (int i = 0; i < 18; ++i) conv<MODE, RELU, G::NG, G::S>(tl, 1, id);
+  for (int i = 0; i < 18; ++i) conv<MODE, RELU, G::S>(tl, 1, id, a, i + 1 < 18);
   store_out(tl, y, n, head<MODE>(tl, 1), H, T);
 }
 
@@ -34,15 +35,16 @@ IP_KERNEL(rrcdnet) {
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, H, n);
   f32x4 id[16];
+  typename Op<MODE>::A a = load_a0<MODE>(tl, 0);
   zero_guards(lds);
   stem<MODE>(tl, 0);
   __syncthreads();
-  for (int i = 0; i < 15; ++i) conv<MODE, RELU, G::NG, G::S>(tl, 1, id);
+  for (int i = 0; i < 15; ++i) conv<MODE, RELU, G::S>(tl, 1, id, a, true);
   const float r = head<MODE>(tl, 2);
   __syncthreads();               // the left stem overwrites the rows the right head just read
   stem<MODE>(tl, 1);
   __syncthreads();
-  for (int i = 0; i < 14; ++i) conv<MODE, RELU, G::NG, G::S>(tl, i == 7 ? 1 : 2, id);
+  for (int i = 0; i < 14; ++i) conv<MODE, RELU, G::S>(tl, i == 7 ? 1 : 2, id, a, i + 1 < 14);
   const float l = head<MODE>(tl, 3);
   const int p = tl.base + (int)threadIdx.x;
   const float xv = in_range(p, L) ? tl.x[p] : 0.f;
@@ -56,14 +58,15 @@ IP_KERNEL(dsdn) {
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, H, n);
   f32x4 id[16];
+  typename Op<MODE>::A a = load_a0<MODE>(tl, 0);
   zero_guards(lds);
   stem<MODE>(tl, 0);
   __syncthreads();
-  conv<MODE, RELU, G::NG, G::S>(tl, 1, id);                       // conv1
-  conv<MODE, RELU | SAVE_ID, G::NG, G::S>(tl, 1, id);             // conv2 -> first block identity
+  conv<MODE, RELU, G::S>(tl, 1, id, a, true);                        // conv1
+  conv<MODE, RELU | SAVE_ID, G::S>(tl, 1, id, a, true);              // conv2 -> first block identity
   for (int b = 0; b < 15; ++b) {
-    conv<MODE, RELU, G::NG, G::S>(tl, 1, id);                     // relu(bn1(conv1 x))
-    conv<MODE, RELU | ADD_ID | SAVE_ID, G::NG, G::S>(tl, 1, id);  // relu(bn2(conv2 .) + x)
+    conv<MODE, RELU, G::S>(tl, 1, id, a, true);                      // relu(bn1(conv1 x))
+    conv<MODE, RELU | ADD_ID | SAVE_ID, G::S>(tl, 1, id, a, b < 14); // relu(bn2(conv2 .) + x)
   }
   store_out(tl, y, n, head<MODE>(tl, 1), H, T);
 }
@@ -75,12 +78,13 @@ IP_KERNEL(pidn) {
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, H, n);
   f32x4 id[16];
+  typename Op<MODE>::A a = load_a0<MODE>(tl, 0);
   zero_guards(lds);
   stem<MODE>(tl, 0);
   __syncthreads();
   for (int b = 0; b < 15; ++b) {
-    conv<MODE, RELU, G::NG, G::S>(tl, 1, id);
-    conv<MODE, 0, G::NG, G::S>(tl, 1, id);
+    conv<MODE, RELU, G::S>(tl, 1, id, a, true);
+    conv<MODE, 0, G::S>(tl, 1, id, a, b < 14);
   }
   stem<MODE, true>(tl, 0);       // + identity (the stem output), recomputed from x
   __syncthreads();

@@ -91,22 +91,15 @@ template <> struct Op<MODE_X3> {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, acc, 0, 0, 0);
   }
   __device__ static void store4(char* act, int prow, int c0, f32x4 v) {
-    bf16x4 hi, lo;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      hi[r] = (__bf16)v[r];
-      lo[r] = (__bf16)(v[r] - bf2f(hi[r]));
-    }
+    const bf16x4 hi = __builtin_convertvector(v, bf16x4);           // 2 x v_cvt_pk_bf16_f32
+    const bf16x4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x4), bf16x4);
     *(bf16x4*)(act + off_f32(prow, 2 * c0)) = hi;
     *(bf16x4*)(act + off_f32(prow, 128 + 2 * c0)) = lo;
   }
   __device__ static f32x4 load4(const char* act, int prow, int c0) {
     const bf16x4 hi = *(const bf16x4*)(act + off_f32(prow, 2 * c0));
     const bf16x4 lo = *(const bf16x4*)(act + off_f32(prow, 128 + 2 * c0));
-    f32x4 v;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = bf2f(hi[r]) + bf2f(lo[r]);
-    return v;
+    return __builtin_convertvector(hi, f32x4) + __builtin_convertvector(lo, f32x4);
   }
 };
 
@@ -126,17 +119,10 @@ template <> struct Op<MODE_B1> {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, acc, 0, 0, 0);
   }
   __device__ static void store4(char* act, int prow, int c0, f32x4 v) {
-    bf16x4 hi;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) hi[r] = (__bf16)v[r];
-    *(bf16x4*)(act + off_f32(prow, 2 * c0)) = hi;
+    *(bf16x4*)(act + off_f32(prow, 2 * c0)) = __builtin_convertvector(v, bf16x4);
   }
   __device__ static f32x4 load4(const char* act, int prow, int c0) {
-    const bf16x4 hi = *(const bf16x4*)(act + off_f32(prow, 2 * c0));
-    f32x4 v;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = bf2f(hi[r]);
-    return v;
+    return __builtin_convertvector(*(const bf16x4*)(act + off_f32(prow, 2 * c0)), f32x4);
   }
 };
 
@@ -203,9 +189,24 @@ __device__ __forceinline__ float head(const Tile& tl, int slot) {
   return a;
 }
 
-// One Conv1d(64,64,3,d): NG N-tiles per pass (weights re-read from L2 per pass), S partial sums.
-template <int MODE, int EPI, int NG, int S>
-__device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16]) {
+// LDS-only workgroup barrier: waits for this wave's LDS traffic, NOT for its outstanding global
+// loads (the prefetched weights stay in flight across it).  One asm statement, so the compiler
+// cannot move memory accesses across the barrier either.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// A-operands of (layer, k-step 0), loaded one k-step ahead of their use (software pipelining):
+// every k-step issues the global (L2) load of the next k-step's weights, and the last k-step of a
+// layer issues the next layer's first one, so no MFMA chain waits on an L2 round trip.
+template <int MODE>
+__device__ __forceinline__ typename Op<MODE>::A load_a0(const Tile& tl, int layer) {
+  const int m = (threadIdx.x >> 6) & 3, lane = threadIdx.x & 63;
+  return Op<MODE>::load_a(tl.big + (size_t)layer * BIG_BYTES, m, 0, lane);
+}
+
+// One Conv1d(64,64,3,d) over the tile; S partial sums per accumulator (k-steps dealt round-robin).
+// `a` holds this layer's k-step-0 A-operand on entry and the next layer's on exit.
+template <int MODE, int EPI, int S>
+__device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], typename Op<MODE>::A& a, bool has_next) {
   using O = Op<MODE>;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int m = w & 3, nh = w >> 2;
@@ -213,65 +214,53 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16]) {
   const uint8_t* wl = tl.big + (size_t)tl.layer * BIG_BYTES;
   const f32x4 bias = *(const f32x4*)(wl + BIAS_OFF + (16 * m + 4 * q) * 4);
 
-  f32x4 fin[16];
+  f32x4 part[S][16];
 #pragma unroll
-  for (int g0 = 0; g0 < 16; g0 += NG) {
-    f32x4 part[S][NG];
+  for (int k = 0; k < S; ++k)
 #pragma unroll
-    for (int k = 0; k < S; ++k)
+    for (int n = 0; n < 16; ++n) part[k][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int n = 0; n < NG; ++n) part[k][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < O::KSTEPS; ++s) {
+    const int t = O::tap(s);
+    const typename O::A cur = a;
+    if (s + 1 < O::KSTEPS) a = O::load_a(wl, m, s + 1, lane);
+    else if (has_next) a = O::load_a(wl + BIG_BYTES, m, 0, lane);
 #pragma unroll
-    for (int s = 0; s < O::KSTEPS; ++s) {
-      const int t = O::tap(s);
-      const typename O::A a = O::load_a(wl, m, s, lane);
-#pragma unroll
-      for (int n = 0; n < NG; ++n) {
-        const int prow = GUARD + nh * 256 + (g0 + n) * 16 + c16 + (t - 1) * dil;
-        const typename O::B b = O::load_b(tl.lds, prow, s, q);
-        part[s % S][n] = O::mma(a, b, part[s % S][n]);
-        // bound how far the scheduler hoists B-fragment reads (VGPR pressure at 2 waves/SIMD)
-        if ((n & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-#pragma unroll
-    for (int n = 0; n < NG; ++n) {
-      f32x4 v = part[0][n];
-#pragma unroll
-      for (int k = 1; k < S; ++k) v += part[k][n];
-      fin[g0 + n] = v;
+    for (int n = 0; n < 16; ++n) {
+      const int prow = GUARD + nh * 256 + n * 16 + c16 + (t - 1) * dil;
+      const typename O::B b = O::load_b(tl.lds, prow, s, q);
+      part[s % S][n] = O::mma(cur, b, part[s % S][n]);
+      // bound how far the scheduler hoists B-fragment reads (VGPR pressure at 2 waves/SIMD)
+      if ((n & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
   }
-  __syncthreads();                 // every read of the layer input is done: overwrite in place
+  lds_barrier();                   // every read of the layer input is done: overwrite in place
+  // rows outside [0, L) are re-zeroed (every reference Conv1d zero-pads); only waves whose 256
+  // rows straddle a spectrum end pay for the per-lane select
+  const int r0 = tl.base + nh * 256;
+  const bool wave_inside = r0 >= 0 && r0 + 256 <= tl.L;
 #pragma unroll
   for (int n = 0; n < 16; ++n) {
     const int row = nh * 256 + n * 16 + c16;
-    const bool valid = in_range(tl.base + row, tl.L);
-    f32x4 v = fin[n] + bias;
-    if (EPI & ADD_ID) v += id[n];
+    f32x4 v = part[0][n];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float x = v[r];
-      if (EPI & RELU) x = fmaxf(x, 0.f);
-      v[r] = valid ? x : 0.f;
-    }
+    for (int k = 1; k < S; ++k) v += part[k][n];
+    v += bias;
+    if (EPI & ADD_ID) v += id[n];
+    if (EPI & RELU) v = __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
+    if (!wave_inside && !in_range(tl.base + row, tl.L)) v = f32x4{0.f, 0.f, 0.f, 0.f};
     if (EPI & SAVE_ID) id[n] = v;
     O::store4(tl.lds, row + GUARD, 16 * m + 4 * q, v);
   }
-  __syncthreads();
+  lds_barrier();
   tl.layer += 1;
 }
 
-// accumulation geometry per mode: F32 splits the fp32 chain 2 ways (128 accumulator VGPRs); X3
-// (error dominated by the operand split) keeps one chain.  The residual net (DSDN) needs 64 VGPRs
-// of identity and keeps one chain.
-template <int MODE, bool RES> struct Geo;
-template <> struct Geo<MODE_F32, false> { static constexpr int NG = 16, S = 2; };
-template <> struct Geo<MODE_F32, true> { static constexpr int NG = 16, S = 1; };
-template <> struct Geo<MODE_X3, false> { static constexpr int NG = 16, S = 1; };
-template <> struct Geo<MODE_X3, true> { static constexpr int NG = 16, S = 1; };
-template <> struct Geo<MODE_B1, false> { static constexpr int NG = 16, S = 1; };
-template <> struct Geo<MODE_B1, true> { static constexpr int NG = 16, S = 1; };
+// partial sums per accumulator: F32 splits the fp32 chain 2 ways (128 accumulator VGPRs); the
+// residual net (DSDN) needs 64 VGPRs of identity and keeps one chain; split-bf16 error is
+// dominated by the operand split, one chain.
+template <int MODE, bool RES> struct Geo { static constexpr int S = 1; };
+template <> struct Geo<MODE_F32, false> { static constexpr int S = 2; };
 
 __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const float* x, int L, int T,
                                           int tiles, int halo, int& n_out) {

@@ -1,0 +1,61 @@
+"""Print the engine-vs-reference error table for every network, weight set, input set and engine dtype.
+
+    python tools/parity_report.py [--out profiles/parity.md]
+
+Needs a GPU.  Reads only the committed fixtures (tests/golden); the same numbers back the bars in
+tests/test_forward_gpu.py and the precision discussion in DESIGN.md.
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fiber-raman-intensity_amd"))
+sys.path.insert(0, ROOT)
+
+from conftest import INPUT_SETS, golden_inputs, golden_state_dict, input_array, load_golden  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    import raman_mi355x as R
+    inp = golden_inputs()
+    rows = ["| network | weights | dtype | max-rel vs fp32 ref (all inputs) | max-abs vs fp32 ref | "
+            "engine vs fp64 forward (rel) | fp32 ref vs fp64 forward (rel) |",
+            "|---|---|---|---|---|---|---|"]
+    for arch in R.MODELS:
+        g = load_golden(arch)
+        whichs = ["synth"] + (["trained"] if any(k.startswith("w::") for k in g.files) else [])
+        for which in whichs:
+            sd = golden_state_dict(arch, which)
+            for dtype in ("fp32", "bf16x3", "bf16"):
+                m = R.MODELS[arch]()
+                m.load_state_dict(sd)
+                m = m.cuda().eval().set_engine_dtype(dtype)
+                rel = ab = ours = theirs = 0.0
+                for name in INPUT_SETS:
+                    x = torch.from_numpy(input_array(inp, name)).unsqueeze(1).cuda()
+                    with torch.no_grad():
+                        y = m(x).squeeze(1).cpu().numpy()
+                    ref, ex = g[f"{which}_{name}"], g[f"f64_{which}_{name}"]
+                    sc = max(np.abs(ref).max(), 1e-30)
+                    rel = max(rel, np.abs(y - ref).max() / sc)
+                    ab = max(ab, np.abs(y - ref).max())
+                    ours = max(ours, np.abs(y - ex).max() / sc)
+                    theirs = max(theirs, np.abs(ref - ex).max() / sc)
+                rows.append(f"| {arch} | {which} | {dtype} | {rel:.2e} | {ab:.2e} | {ours:.2e} | {theirs:.2e} |")
+                print(rows[-1], flush=True)
+    text = "\n".join(rows) + "\n"
+    if args.out:
+        with open(args.out, "w") as fh:
+            fh.write(text)
+
+
+if __name__ == "__main__":
+    main()
