@@ -235,8 +235,8 @@ __global__ __launch_bounds__(THREADS) void segment(const uint8_t* __restrict__ b
   Tile tl = make_tile(lds, blob, x, L, T, tiles, sg.halo, n);
   tl.layer = sg.layer0;
   f32x4 id[16];
-  typename Op<MODE>::A a;
-  if (sg.n_convs) a = load_a0<MODE>(tl, sg.layer0);
+  LayerA<MODE> a;
+  if (sg.n_convs) load_layer_a<MODE>(tl, sg.layer0, a);
   zero_guards(lds);
   if (sg.pro == PRO_STEM) prologue_stem<MODE>(tl, sg, n);
   else prologue_cbam<MODE>(tl, sg, n);

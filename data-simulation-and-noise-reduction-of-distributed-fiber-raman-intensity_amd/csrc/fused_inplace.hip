@@ -20,7 +20,8 @@ IP_KERNEL(denoisecnn) {
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, H, n);
   f32x4 id[16];
-  typename Op<MODE>::A a = load_a0<MODE>(tl, 0);
+  LayerA<MODE> a;
+  load_layer_a<MODE>(tl, 0, a);
   zero_guards(lds);
   stem<MODE>(tl, 0);
   __syncthreads();
@@ -35,7 +36,8 @@ IP_KERNEL(rrcdnet) {
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, H, n);
   f32x4 id[16];
-  typename Op<MODE>::A a = load_a0<MODE>(tl, 0);
+  LayerA<MODE> a;
+  load_layer_a<MODE>(tl, 0, a);
   zero_guards(lds);
   stem<MODE>(tl, 0);
   __syncthreads();
@@ -58,7 +60,8 @@ IP_KERNEL(dsdn) {
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, H, n);
   f32x4 id[16];
-  typename Op<MODE>::A a = load_a0<MODE>(tl, 0);
+  LayerA<MODE> a;
+  load_layer_a<MODE>(tl, 0, a);
   zero_guards(lds);
   stem<MODE>(tl, 0);
   __syncthreads();
@@ -78,7 +81,8 @@ IP_KERNEL(pidn) {
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, H, n);
   f32x4 id[16];
-  typename Op<MODE>::A a = load_a0<MODE>(tl, 0);
+  LayerA<MODE> a;
+  load_layer_a<MODE>(tl, 0, a);
   zero_guards(lds);
   stem<MODE>(tl, 0);
   __syncthreads();

@@ -58,6 +58,17 @@ template <> struct Op<MODE_F32> {
     return B{*(const f32x4*)(act + off_f32(prow, 64 * g + 16 * q))};
   }
   __device__ static int tap(int s) { return s >> 2; }
+  // precomputed-address forms: PLANES byte addresses per k-step / store, plus a row offset that
+  // is a multiple of 16 rows (leaves the row swizzle unchanged -> ds_* immediate offsets)
+  static constexpr int PLANES = 1;
+  __device__ static int bslot(int s, int q, int) { return 4 * (s & 3) + q; }
+  __device__ static int sbyte(int c0, int) { return 4 * c0; }
+  __device__ static B load_b_at(const char* act, const uint32_t (&ad)[PLANES], uint32_t off) {
+    return B{*(const f32x4*)(act + ad[0] + off)};
+  }
+  __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v) {
+    *(f32x4*)(act + ad[0] + off) = v;
+  }
   __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w[i], b.v[i], acc, 0, 0, 0);
@@ -85,6 +96,18 @@ template <> struct Op<MODE_X3> {
              *(const bf16x8*)(act + off_f32(prow, 128 + 64 * u + 16 * q))};
   }
   __device__ static int tap(int s) { return s >> 1; }
+  static constexpr int PLANES = 2;
+  __device__ static int bslot(int s, int q, int p) { return 8 * p + 4 * (s & 1) + q; }
+  __device__ static int sbyte(int c0, int p) { return 128 * p + 2 * c0; }
+  __device__ static B load_b_at(const char* act, const uint32_t (&ad)[PLANES], uint32_t off) {
+    return B{*(const bf16x8*)(act + ad[0] + off), *(const bf16x8*)(act + ad[1] + off)};
+  }
+  __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v) {
+    const bf16x4 hi = __builtin_convertvector(v, bf16x4);
+    const bf16x4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x4), bf16x4);
+    *(bf16x4*)(act + ad[0] + off) = hi;
+    *(bf16x4*)(act + ad[1] + off) = lo;
+  }
   __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo, b.hi, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, acc, 0, 0, 0);
@@ -115,6 +138,15 @@ template <> struct Op<MODE_B1> {
     return B{*(const bf16x8*)(act + off_f32(prow, 64 * (s & 1) + 16 * q))};
   }
   __device__ static int tap(int s) { return s >> 1; }
+  static constexpr int PLANES = 1;
+  __device__ static int bslot(int s, int q, int) { return 4 * (s & 1) + q; }
+  __device__ static int sbyte(int c0, int) { return 2 * c0; }
+  __device__ static B load_b_at(const char* act, const uint32_t (&ad)[PLANES], uint32_t off) {
+    return B{*(const bf16x8*)(act + ad[0] + off)};
+  }
+  __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v) {
+    *(bf16x4*)(act + ad[0] + off) = __builtin_convertvector(v, bf16x4);
+  }
   __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, acc, 0, 0, 0);
   }
@@ -194,65 +226,154 @@ __device__ __forceinline__ float head(const Tile& tl, int slot) {
 // cannot move memory accesses across the barrier either.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// A-operands of (layer, k-step 0), loaded one k-step ahead of their use (software pipelining):
-// every k-step issues the global (L2) load of the next k-step's weights, and the last k-step of a
-// layer issues the next layer's first one, so no MFMA chain waits on an L2 round trip.
+// Work split of one layer (512 rows x 64 couts) over the 8 waves: wave w owns the M-tile pair
+// {2mp, 2mp+1} (mp = w & 1, 32 couts) and, in each of the 4 row blocks of 128, the 32 rows
+// 128j + 32nq + [0, 32) (nq = w >> 1, 2 N-tiles).  Every B fragment read from LDS feeds both
+// M-tiles (2 x 3 split-bf16 MFMAs), so each activation row is read by 2 waves, not 4.
+constexpr int IP_MT = 2, IP_NT = 2, IP_NB = 4, IP_BR = WB / IP_NB;
+
+// A-operands (this wave's weights) of a whole layer: [M-tile][k-step].  Loaded once per layer
+// from L2 (the four waves of a pair hit the same lines at the same time: mostly L1 hits); the
+// next layer's k-step s is fetched right after its last use in the current layer.
 template <int MODE>
-__device__ __forceinline__ typename Op<MODE>::A load_a0(const Tile& tl, int layer) {
-  const int m = (threadIdx.x >> 6) & 3, lane = threadIdx.x & 63;
-  return Op<MODE>::load_a(tl.big + (size_t)layer * BIG_BYTES, m, 0, lane);
+using LayerA = typename Op<MODE>::A[IP_MT][Op<MODE>::KSTEPS];
+
+template <int MODE>
+__device__ __forceinline__ void load_layer_a(const Tile& tl, int layer, LayerA<MODE>& a) {
+  const int mp = (threadIdx.x >> 6) & 1, lane = threadIdx.x & 63;
+  const uint8_t* wl = tl.big + (size_t)layer * BIG_BYTES;
+#pragma unroll
+  for (int mm = 0; mm < IP_MT; ++mm)
+#pragma unroll
+    for (int s = 0; s < Op<MODE>::KSTEPS; ++s) a[mm][s] = Op<MODE>::load_a(wl, IP_MT * mp + mm, s, lane);
 }
 
-// One Conv1d(64,64,3,d) over the tile; S partial sums per accumulator (k-steps dealt round-robin).
-// `a` holds this layer's k-step-0 A-operand on entry and the next layer's on exit.
+// One Conv1d(64,64,3,d) over the tile, updated in place with a one-block lag.
+//
+// Block j reads input rows down to 128j - d, i.e. the tail of block j-1, so block j-1's outputs
+// may overwrite their rows only once EVERY wave has finished block j: the barrier after block j.
+// They are then written while block j+1 computes (after its first k-step), so the LDS stores and
+// their epilogue VALU overlap the MFMA stream instead of forming a separate write phase.
+// Sequence: C0 | C1 | S0+C2 | S1+C3 | S2 S3 |.   id[16] = [block][N-tile][M-tile] identities.
 template <int MODE, int EPI, int S>
-__device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], typename Op<MODE>::A& a, bool has_next) {
+__device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], LayerA<MODE>& a, bool has_next) {
   using O = Op<MODE>;
+  constexpr int NB = IP_NB, NT = IP_NT, MT = IP_MT, BR = IP_BR;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int m = w & 3, nh = w >> 2;
+  const int mp = w & 1, nq = w >> 1;
   const int q = lane >> 4, c16 = lane & 15;
-  const uint8_t* wl = tl.big + (size_t)tl.layer * BIG_BYTES;
-  const f32x4 bias = *(const f32x4*)(wl + BIAS_OFF + (16 * m + 4 * q) * 4);
+  const uint8_t* wcur = tl.big + (size_t)tl.layer * BIG_BYTES;
+  const uint8_t* wnext = wcur + BIG_BYTES;
+  f32x4 bias[MT];
+#pragma unroll
+  for (int mm = 0; mm < MT; ++mm) bias[mm] = *(const f32x4*)(wcur + BIAS_OFF + (16 * (MT * mp + mm) + 4 * q) * 4);
 
-  f32x4 part[S][16];
-#pragma unroll
-  for (int k = 0; k < S; ++k)
-#pragma unroll
-    for (int n = 0; n < 16; ++n) part[k][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // LDS byte addresses of this lane's B fragments for every k-step (row = first row of the wave's
+  // share of block 0), and of its output stores; blocks and N-tiles add multiples of 16 rows,
+  // which leave the row swizzle unchanged (-> ds_* immediate offsets).
+  uint32_t badr[O::KSTEPS][O::PLANES], sadr[MT][O::PLANES];
+  const int prow0 = GUARD + (BR / 4) * nq + c16;
 #pragma unroll
   for (int s = 0; s < O::KSTEPS; ++s) {
-    const int t = O::tap(s);
-    const typename O::A cur = a;
-    if (s + 1 < O::KSTEPS) a = O::load_a(wl, m, s + 1, lane);
-    else if (has_next) a = O::load_a(wl + BIG_BYTES, m, 0, lane);
+    const int pr = prow0 + (O::tap(s) - 1) * dil;
 #pragma unroll
-    for (int n = 0; n < 16; ++n) {
-      const int prow = GUARD + nh * 256 + n * 16 + c16 + (t - 1) * dil;
-      const typename O::B b = O::load_b(tl.lds, prow, s, q);
-      part[s % S][n] = O::mma(cur, b, part[s % S][n]);
-      // bound how far the scheduler hoists B-fragment reads (VGPR pressure at 2 waves/SIMD)
-      if ((n & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    for (int p = 0; p < O::PLANES; ++p) badr[s][p] = pr * ROWB_F32 + ((O::bslot(s, q, p) ^ swz256(pr)) << 4);
+  }
+#pragma unroll
+  for (int mm = 0; mm < MT; ++mm)
+#pragma unroll
+    for (int p = 0; p < O::PLANES; ++p) {
+      const int b = O::sbyte(16 * (MT * mp + mm) + 4 * q, p);
+      sadr[mm][p] = prow0 * ROWB_F32 + ((((b >> 4) ^ swz256(prow0)) << 4) | (b & 15));
     }
-  }
-  lds_barrier();                   // every read of the layer input is done: overwrite in place
-  // rows outside [0, L) are re-zeroed (every reference Conv1d zero-pads); only waves whose 256
-  // rows straddle a spectrum end pay for the per-lane select
-  const int r0 = tl.base + nh * 256;
-  const bool wave_inside = r0 >= 0 && r0 + 256 <= tl.L;
+
+  f32x4 res[NB][NT][MT];
+  auto store_block = [&](int j) {
+    const int rb = BR * j + (BR / 4) * nq;            // first row of this wave's share of block j
+    const bool inside = tl.base + rb >= 0 && tl.base + rb + BR / 4 <= tl.L;
 #pragma unroll
-  for (int n = 0; n < 16; ++n) {
-    const int row = nh * 256 + n * 16 + c16;
-    f32x4 v = part[0][n];
+    for (int i = 0; i < NT; ++i) {
+      const int row = rb + 16 * i + c16;
+      const bool zero = !inside && !in_range(tl.base + row, tl.L);       // conv zero padding
 #pragma unroll
-    for (int k = 1; k < S; ++k) v += part[k][n];
-    v += bias;
-    if (EPI & ADD_ID) v += id[n];
-    if (EPI & RELU) v = __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
-    if (!wave_inside && !in_range(tl.base + row, tl.L)) v = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (EPI & SAVE_ID) id[n] = v;
-    O::store4(tl.lds, row + GUARD, 16 * m + 4 * q, v);
+      for (int mm = 0; mm < MT; ++mm) {
+        f32x4 v = res[j][i][mm] + bias[mm];
+        if (EPI & ADD_ID) v += id[(j * NT + i) * MT + mm];
+        if (EPI & RELU) v = __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
+        if (zero) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
+#if defined(RDN_ABLATE_NOSTORE)
+        if (v[0] == 123456.f)
+#endif
+        O::store4_at(tl.lds, sadr[mm], (uint32_t)(BR * j + 16 * i) * ROWB_F32, v);
+      }
+    }
+  };
+
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    f32x4 part[S][NT][MT];
+#pragma unroll
+    for (int k = 0; k < S; ++k)
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int mm = 0; mm < MT; ++mm) part[k][i][mm] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // B fragments are software-pipelined one k-step ahead: the reads for k-step s+1 are issued
+    // before the MFMAs of k-step s, so LDS latency hides under 2 x 3 x 16-cycle MFMA chains.
+    typename O::B bnext[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) bnext[i] = O::load_b_at(tl.lds, badr[0], (uint32_t)(BR * j + 16 * i) * ROWB_F32);
+#pragma unroll
+    for (int s = 0; s < O::KSTEPS; ++s) {
+      typename O::B bcur[NT];
+#pragma unroll
+      for (int i = 0; i < NT; ++i) bcur[i] = bnext[i];
+      if (s + 1 < O::KSTEPS) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+#if defined(RDN_ABLATE_NOLDS)          // diagnostic builds only (tools/ablate.py): reuse block reads
+          bnext[i] = bcur[i];
+          asm volatile("" : "+v"(bnext[i].hi) ::);
+#else
+          bnext[i] = O::load_b_at(tl.lds, badr[s + 1], (uint32_t)(BR * j + 16 * i) * ROWB_F32);
+#endif
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const typename O::B& b = bcur[i];
+#pragma unroll
+        for (int mm = 0; mm < MT; ++mm) {
+#if defined(RDN_ABLATE_NOMFMA)
+          part[s % S][i][mm] += *(const f32x4*)&b;
+#else
+          part[s % S][i][mm] = O::mma(a[mm][s], b, part[s % S][i][mm]);
+#endif
+        }
+      }
+      if (j == NB - 1 && has_next) {                                   // last use of a[.][s]
+#pragma unroll
+        for (int mm = 0; mm < MT; ++mm) a[mm][s] = O::load_a(wnext, MT * mp + mm, s, lane);
+      }
+      if (s == 0 && j >= 2) store_block(j - 2);                        // lagged write-back
+      // keep B-fragment reads within their k-step (VGPR budget of 2 waves/SIMD)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int mm = 0; mm < MT; ++mm) {
+        f32x4 v = part[0][i][mm];
+#pragma unroll
+        for (int k = 1; k < S; ++k) v += part[k][i][mm];
+        res[j][i][mm] = v;
+      }
+    lds_barrier();                 // every wave is done reading the rows block j needed
   }
-  lds_barrier();
+  store_block(NB - 2);
+  store_block(NB - 1);
+  lds_barrier();                   // the layer's output is complete
   tl.layer += 1;
 }
 

@@ -1,0 +1,82 @@
+"""Diagnostic ablation of the in-place kernels (not part of the product).
+
+Builds libraman_mi355x variants with RDN_ABLATE_* / RDN_IP_NB macros into /tmp and times the RRCDNet
+forward of each in ONE process (interleaved rounds), so the deltas say which resource bounds the
+kernel: MFMA issue (NOLDS), LDS traffic (NOMFMA), the write-back (NOSTORE).
+
+    python tools/ablate.py build      # in the build container (hipcc)
+    python tools/ablate.py run        # on the GPU box
+"""
+import ctypes
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fiber-raman-intensity_amd", "csrc")
+OUT = os.path.join(ROOT, "tools", "ablate_build")
+VARIANTS = {"base": "", "nolds": "-DRDN_ABLATE_NOLDS", "nomfma": "-DRDN_ABLATE_NOMFMA",
+            "nostore": "-DRDN_ABLATE_NOSTORE", "nb8": "-DRDN_IP_NB=8", "nb2": "-DRDN_IP_NB=2"}
+
+
+def build():
+    import torch
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    os.makedirs(OUT, exist_ok=True)
+    srcs = ["fused_bf16.hip", "fused_inplace.hip", "cbam.hip", "generator.hip", "metrics.hip", "abi.cpp", "pack.cpp"]
+    for name, flag in VARIANTS.items():
+        objs = []
+        for s in srcs:
+            o = os.path.join(OUT, f"{name}_{s}.o")
+            cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mcode-object-version=5",
+                   "-fno-gpu-rdc", "-c", os.path.join(CSRC, s), "-o", o] + ([flag] if flag else [])
+            subprocess.run(cmd, check=True, cwd=CSRC)
+            objs.append(o)
+        subprocess.run(["g++", "-shared", "-o", os.path.join(OUT, f"lib_{name}.so")] + objs +
+                       [f"-L{tlib}", "-l:libamdhip64.so", f"-Wl,-rpath,{tlib}"], check=True)
+        print("built", name, flush=True)
+
+
+def run():
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fiber-raman-intensity_amd"))
+    import raman_mi355x as R
+    from raman_mi355x import _lib, engine
+    dev = torch.device("cuda")
+    B, L = 2048, 10000
+    clean, noisy, _, _ = engine.generate(B, 1, signal_length=L, device=dev)
+    x = noisy.view(B, 1, L)
+    y = torch.empty_like(x)
+    torch.manual_seed(0)
+    model = R.RRCDNet()
+    libs = {}
+    for name in VARIANTS:
+        lib = ctypes.CDLL(os.path.join(OUT, f"lib_{name}.so"))
+        for fn, (args, res) in _lib._SIGNATURES.items():
+            getattr(lib, fn).argtypes = args
+            getattr(lib, fn).restype = res
+        libs[name] = lib
+    results = {}
+    for dtype in sys.argv[2:] or ["bf16x3", "fp32"]:
+        packed = engine.pack("RRCDNet", model.state_dict(), dtype, dev)
+        code = engine.DTYPE_ID[dtype]
+        times = {k: [] for k in libs}
+        for rnd in range(4):
+            for name, lib in libs.items():
+                stream = torch.cuda.current_stream().cuda_stream
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                lib.rdn_forward(1, code, packed.data_ptr(), x.data_ptr(), y.data_ptr(), B, L, None, 0, stream)
+                e0.record()
+                for _ in range(3):
+                    rc = lib.rdn_forward(1, code, packed.data_ptr(), x.data_ptr(), y.data_ptr(), B, L, None, 0, stream)
+                    assert rc == 0, lib.rdn_last_error()
+                e1.record()
+                torch.cuda.synchronize()
+                times[name].append(e0.elapsed_time(e1) / 3)
+        for name, t in times.items():
+            results[(dtype, name)] = min(t)
+            print(f"{dtype:7s} {name:8s} {min(t):8.2f} ms  ({B / min(t) * 1e3:9.0f} spectra/s)", flush=True)
+
+
+if __name__ == "__main__":
+    {"build": build, "run": run}[sys.argv[1]]()
