@@ -43,6 +43,15 @@ constexpr int BIG_BYTES_BF16 = BIG_FRAG_BYTES_BF16 + C * 4;                // 24
 constexpr int BIG_FRAG_FLOATS_F32 = 4 * 12 * 64 * 4;                       // 12288
 constexpr int BIG_BYTES_F32 = (BIG_FRAG_FLOATS_F32 + C) * 4;               // 49408
 
+// 16-bit single-rounding layout of fused16.hip (RDN_BF16, non-CBAM networks): the same
+// [m 4][kstep 6][lane 64][8] fragments + bias, but with the K order permuted so that element j of
+// lane quarter q in k-step (t, u) is cin = h16_channel(4u + q, j) — the channel held by element j
+// of 16-B slot 4u + q of an LDS activation row (fused16.hip header).
+__host__ __device__ constexpr int h16_channel(int slot, int j) {
+  return 32 * (slot >> 2) + 4 * (slot & 3) + (j & 3) + 16 * (j >> 2);
+}
+constexpr int H16_WB = 640;      // rows per fused16 tile (two 80 KiB ping-pong buffers)
+
 // ---- LDS image ------------------------------------------------------------------------------
 // bf16 activation buffer: ROWS x 128 B, 16-B slots XOR-swizzled by (row & 7): conflict-free
 // ds_read_b128 B-fragment reads for any row offset, 2-way ds_write_b64 epilogue stores.

@@ -334,7 +334,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], LayerA<
         for (int i = 0; i < NT; ++i) {
 #if defined(RDN_ABLATE_NOLDS)          // diagnostic builds only (tools/ablate.py): reuse block reads
           bnext[i] = bcur[i];
-          asm volatile("" : "+v"(bnext[i].hi) ::);
+          asm volatile("" : "+v"(reinterpret_cast<f32x4&>(bnext[i])) ::);
 #else
           bnext[i] = O::load_b_at(tl.lds, badr[s + 1], (uint32_t)(BR * j + 16 * i) * ROWB_F32);
 #endif

@@ -203,7 +203,11 @@ static void pack_big_bf16(const Folded& f, uint8_t* dst) {
       for (int lane = 0; lane < 64; ++lane)
         for (int j = 0; j < 8; ++j) {
           const int t = s >> 1, u = s & 1;
+#if defined(RDN_BF16_LEGACY)
           const int co = 16 * m + (lane & 15), ci = 32 * u + 8 * (lane >> 4) + j;
+#else
+          const int co = 16 * m + (lane & 15), ci = h16_channel(4 * u + (lane >> 4), j);
+#endif
           const double v = co < f.cout ? f.W(co, ci, t) : 0.0;
           frag[(((m * 6 + s) * 64) + lane) * 8 + j] = to_bf16(v);
         }

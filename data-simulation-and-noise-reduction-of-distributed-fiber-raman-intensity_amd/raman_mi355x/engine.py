@@ -88,6 +88,8 @@ def forward(arch, dtype, packed, x, out=None):
     y = torch.empty_like(x) if out is None else out
     if y.shape != x.shape or not y.is_contiguous() or y.device != x.device:
         raise ValueError("out must be a contiguous tensor like the input")
+    if y.data_ptr() < x.data_ptr() + x.numel() * 4 and x.data_ptr() < y.data_ptr() + y.numel() * 4:
+        raise ValueError("out must not overlap the input (tiles re-read input halos while outputs are written)")
     ws_bytes = ctypes.c_size_t()
     L_ = _lib.lib()
     _lib.check(L_.rdn_workspace_size(_arch(arch), _dtype(dtype), n, L, ctypes.byref(ws_bytes)), "rdn_workspace_size")

@@ -115,12 +115,15 @@ def test_pack_layout_rrcdnet(dtype):
                     np.testing.assert_array_equal(frag[m, tg, :, i], exp)
         np.testing.assert_array_equal(L[49152:49408].view(np.float32), b)
     elif dtype == "bf16":
+        # fused16.hip K order: element j of lane quarter q in k-step (t, u) is channel
+        # 32u + 4q + (j & 3) + 16 (j >> 2) (common.hpp h16_channel)
         frag = L[:24576].view(np.uint16).reshape(4, 6, 64, 8)
         for m in range(4):
             for s in range(6):
                 t, u = s >> 1, s & 1
                 for j in range(8):
-                    exp = w[16 * m + (lane & 15), 32 * u + 8 * (lane >> 4) + j, t]
+                    cin = 32 * u + 4 * (lane >> 4) + (j & 3) + 16 * (j >> 2)
+                    exp = w[16 * m + (lane & 15), cin, t]
                     np.testing.assert_array_equal(frag[m, s, :, j], _f32_to_bf16(exp))
         np.testing.assert_array_equal(L[24576:24832].view(np.float32), b)
     else:

@@ -15,21 +15,29 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fiber-raman-intensity_amd", "csrc")
 OUT = os.path.join(ROOT, "tools", "ablate_build")
-VARIANTS = {"base": "", "nolds": "-DRDN_ABLATE_NOLDS", "nomfma": "-DRDN_ABLATE_NOMFMA",
-            "nostore": "-DRDN_ABLATE_NOSTORE", "nb8": "-DRDN_IP_NB=8", "nb2": "-DRDN_IP_NB=2"}
+VARIANTS = {"base": "", "legacy16": "-DRDN_BF16_LEGACY", "nolds": "-DRDN_ABLATE_NOLDS", "nomfma": "-DRDN_ABLATE_NOMFMA",
+            "nostore": "-DRDN_ABLATE_NOSTORE", "noaload": "-DRDN_ABLATE_NOALOAD", "pf3": "-DRDN_H16_PF=3", "ieee": ""}
 
 
 def build():
     import torch
     tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
     os.makedirs(OUT, exist_ok=True)
-    srcs = ["fused_bf16.hip", "fused_inplace.hip", "cbam.hip", "generator.hip", "metrics.hip", "abi.cpp", "pack.cpp"]
+    srcs = ["fused16.hip", "fused_bf16.hip", "fused_inplace.hip", "cbam.hip", "generator.hip", "metrics.hip", "abi.cpp",
+            "pack.cpp"]
+    only = sys.argv[2:]
     for name, flag in VARIANTS.items():
+        if only and name not in only:
+            continue
         objs = []
         for s in srcs:
             o = os.path.join(OUT, f"{name}_{s}.o")
             cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mcode-object-version=5",
-                   "-fno-gpu-rdc", "-c", os.path.join(CSRC, s), "-o", o] + ([flag] if flag else [])
+                   "-fno-gpu-rdc", "-c", os.path.join(CSRC, s), "-o", o] + flag.split()
+            if s in ("fused16.hip", "fused_bf16.hip", "fused_inplace.hip", "cbam.hip") and name != "ieee":
+                cmd += ["-fno-honor-nans", "-mno-amdgpu-ieee"]
+            if s == "generator.hip":
+                cmd += ["-ffp-contract=off"]
             subprocess.run(cmd, check=True, cwd=CSRC)
             objs.append(o)
         subprocess.run(["g++", "-shared", "-o", os.path.join(OUT, f"lib_{name}.so")] + objs +
@@ -51,31 +59,53 @@ def run():
     model = R.RRCDNet()
     libs = {}
     for name in VARIANTS:
+        if not os.path.exists(os.path.join(OUT, f"lib_{name}.so")):
+            continue
         lib = ctypes.CDLL(os.path.join(OUT, f"lib_{name}.so"))
         for fn, (args, res) in _lib._SIGNATURES.items():
             getattr(lib, fn).argtypes = args
             getattr(lib, fn).restype = res
         libs[name] = lib
     results = {}
+    names = engine.param_names("RRCDNet")
+    sd = model.state_dict()
+    host = [sd[k].detach().float().contiguous() for k in names]
+    ptrs = (ctypes.c_void_p * len(host))(*[t.data_ptr() for t in host])
+    numels = (ctypes.c_int64 * len(host))(*[t.numel() for t in host])
+
+    def pack_with(lib, code):
+        size = ctypes.c_size_t()
+        assert lib.rdn_packed_size(1, code, ctypes.byref(size)) == 0
+        blob = torch.empty(size.value, dtype=torch.uint8)
+        rc = lib.rdn_pack(1, code, ptrs, numels, len(host), ctypes.c_void_p(blob.data_ptr()), size.value)
+        assert rc == 0, lib.rdn_last_error()
+        return blob.to(dev)
+
     for dtype in sys.argv[2:] or ["bf16x3", "fp32"]:
-        packed = engine.pack("RRCDNet", model.state_dict(), dtype, dev)
         code = engine.DTYPE_ID[dtype]
+        packed = {name: pack_with(lib, code) for name, lib in libs.items()}
         times = {k: [] for k in libs}
+        outs = {}
         for rnd in range(4):
             for name, lib in libs.items():
                 stream = torch.cuda.current_stream().cuda_stream
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                lib.rdn_forward(1, code, packed.data_ptr(), x.data_ptr(), y.data_ptr(), B, L, None, 0, stream)
+                lib.rdn_forward(1, code, packed[name].data_ptr(), x.data_ptr(), y.data_ptr(), B, L, None, 0, stream)
                 e0.record()
                 for _ in range(3):
-                    rc = lib.rdn_forward(1, code, packed.data_ptr(), x.data_ptr(), y.data_ptr(), B, L, None, 0, stream)
+                    rc = lib.rdn_forward(1, code, packed[name].data_ptr(), x.data_ptr(), y.data_ptr(), B, L, None, 0, stream)
                     assert rc == 0, lib.rdn_last_error()
                 e1.record()
                 torch.cuda.synchronize()
                 times[name].append(e0.elapsed_time(e1) / 3)
+                if rnd == 0:
+                    outs[name] = y[:64].clone()
+        ref = outs.get("base")
         for name, t in times.items():
             results[(dtype, name)] = min(t)
-            print(f"{dtype:7s} {name:8s} {min(t):8.2f} ms  ({B / min(t) * 1e3:9.0f} spectra/s)", flush=True)
+            diff = float((outs[name] - ref).abs().max()) if ref is not None else float("nan")
+            print(f"{dtype:7s} {name:9s} {min(t):8.2f} ms  ({B / min(t) * 1e3:9.0f} spectra/s)  max|y-base| {diff:.3e}",
+                  flush=True)
 
 
 if __name__ == "__main__":
