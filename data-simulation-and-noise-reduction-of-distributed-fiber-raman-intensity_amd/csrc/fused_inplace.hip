@@ -8,93 +8,98 @@
 namespace rdn {
 namespace ip {
 
-#define IP_KERNEL(name) \
-  template <int MODE>   \
-  __global__ __launch_bounds__(THREADS) void name(const uint8_t* __restrict__ blob, const float* __restrict__ x, \
-                                                 float* __restrict__ y, int L, int T, int tiles)
+// Network bodies.  EDGE: the tile holds positions outside [0, L) (first / last tile of a
+// spectrum), whose rows every write-back re-zeroes; interior tiles skip that per-row select.
+#define IP_BODY(name) \
+  template <int MODE, bool EDGE> \
+  __device__ __forceinline__ void name##_body(Tile& tl, float* y, int n, int L, int T)
 
-IP_KERNEL(denoisecnn) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
+IP_BODY(denoisecnn) {
   constexpr int H = fused_halo(DENOISECNN);
   using G = Geo<MODE, false>;
-  int n;
-  Tile tl = make_tile(lds, blob, x, L, T, tiles, H, n);
   f32x4 id[16];
   LayerA<MODE> a;
   load_layer_a<MODE>(tl, 0, a);
-  zero_guards(lds);
+  zero_guards(tl.lds);
   stem<MODE>(tl, 0);
   __syncthreads();
-  for (int i = 0; i < 18; ++i) conv<MODE, RELU, G::S>(tl, 1, id, a, i + 1 < 18);
+  for (int i = 0; i < 18; ++i) conv<MODE, RELU, G::S, EDGE>(tl, 1, id, a, i + 1 < 18);
   store_out(tl, y, n, head<MODE>(tl, 1), H, T);
 }
 
-IP_KERNEL(rrcdnet) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
+IP_BODY(rrcdnet) {
   constexpr int H = fused_halo(RRCDNET);
   using G = Geo<MODE, false>;
-  int n;
-  Tile tl = make_tile(lds, blob, x, L, T, tiles, H, n);
   f32x4 id[16];
   LayerA<MODE> a;
   load_layer_a<MODE>(tl, 0, a);
-  zero_guards(lds);
+  zero_guards(tl.lds);
   stem<MODE>(tl, 0);
   __syncthreads();
-  for (int i = 0; i < 15; ++i) conv<MODE, RELU, G::S>(tl, 1, id, a, true);
+  for (int i = 0; i < 15; ++i) conv<MODE, RELU, G::S, EDGE>(tl, 1, id, a, true);
   const float r = head<MODE>(tl, 2);
   __syncthreads();               // the left stem overwrites the rows the right head just read
   stem<MODE>(tl, 1);
   __syncthreads();
-  for (int i = 0; i < 14; ++i) conv<MODE, RELU, G::S>(tl, i == 7 ? 1 : 2, id, a, i + 1 < 14);
+  for (int i = 0; i < 14; ++i) conv<MODE, RELU, G::S, EDGE>(tl, i == 7 ? 1 : 2, id, a, i + 1 < 14);
   const float l = head<MODE>(tl, 3);
   const int p = tl.base + (int)threadIdx.x;
   const float xv = in_range(p, L) ? tl.x[p] : 0.f;
   store_out(tl, y, n, xv - (r + l) / 2.0f, H, T);
 }
 
-IP_KERNEL(dsdn) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
+IP_BODY(dsdn) {
   constexpr int H = fused_halo(DSDN);
   using G = Geo<MODE, true>;
-  int n;
-  Tile tl = make_tile(lds, blob, x, L, T, tiles, H, n);
   f32x4 id[16];
   LayerA<MODE> a;
   load_layer_a<MODE>(tl, 0, a);
-  zero_guards(lds);
+  zero_guards(tl.lds);
   stem<MODE>(tl, 0);
   __syncthreads();
-  conv<MODE, RELU, G::S>(tl, 1, id, a, true);                        // conv1
-  conv<MODE, RELU | SAVE_ID, G::S>(tl, 1, id, a, true);              // conv2 -> first block identity
+  conv<MODE, RELU, G::S, EDGE>(tl, 1, id, a, true);                        // conv1
+  conv<MODE, RELU | SAVE_ID, G::S, EDGE>(tl, 1, id, a, true);              // conv2 -> first block identity
   for (int b = 0; b < 15; ++b) {
-    conv<MODE, RELU, G::S>(tl, 1, id, a, true);                      // relu(bn1(conv1 x))
-    conv<MODE, RELU | ADD_ID | SAVE_ID, G::S>(tl, 1, id, a, b < 14); // relu(bn2(conv2 .) + x)
+    conv<MODE, RELU, G::S, EDGE>(tl, 1, id, a, true);                      // relu(bn1(conv1 x))
+    conv<MODE, RELU | ADD_ID | SAVE_ID, G::S, EDGE>(tl, 1, id, a, b < 14); // relu(bn2(conv2 .) + x)
   }
   store_out(tl, y, n, head<MODE>(tl, 1), H, T);
 }
 
-IP_KERNEL(pidn) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
+IP_BODY(pidn) {
   constexpr int H = fused_halo(PIDN);
   using G = Geo<MODE, false>;
-  int n;
-  Tile tl = make_tile(lds, blob, x, L, T, tiles, H, n);
   f32x4 id[16];
   LayerA<MODE> a;
   load_layer_a<MODE>(tl, 0, a);
-  zero_guards(lds);
+  zero_guards(tl.lds);
   stem<MODE>(tl, 0);
   __syncthreads();
   for (int b = 0; b < 15; ++b) {
-    conv<MODE, RELU, G::S>(tl, 1, id, a, true);
-    conv<MODE, 0, G::S>(tl, 1, id, a, b < 14);
+    conv<MODE, RELU, G::S, EDGE>(tl, 1, id, a, true);
+    conv<MODE, 0, G::S, EDGE>(tl, 1, id, a, b < 14);
   }
   stem<MODE, true>(tl, 0);       // + identity (the stem output), recomputed from x
   __syncthreads();
   const float v = head<MODE>(tl, 1);
   store_out(tl, y, n, 1.0f / (1.0f + expf(-v)), H, T);
 }
+
+#define IP_KERNEL(name, arch)                                                                              \
+  template <int MODE>                                                                                      \
+  __global__ __launch_bounds__(THREADS) void name(const uint8_t* __restrict__ blob, const float* __restrict__ x, \
+                                                 float* __restrict__ y, int L, int T, int tiles) {          \
+    extern __shared__ __attribute__((aligned(16))) char lds[];                                             \
+    int n;                                                                                                 \
+    Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(arch), n);                                   \
+    if (tl.base >= 0 && tl.base + WB <= L) name##_body<MODE, false>(tl, y, n, L, T);                       \
+    else name##_body<MODE, true>(tl, y, n, L, T);                                                          \
+  }
+
+IP_KERNEL(denoisecnn, DENOISECNN)
+IP_KERNEL(rrcdnet, RRCDNET)
+IP_KERNEL(dsdn, DSDN)
+IP_KERNEL(pidn, PIDN)
 
 }  // namespace ip
 

@@ -103,8 +103,13 @@ template <> struct Op<MODE_X3> {
     return B{*(const bf16x8*)(act + ad[0] + off), *(const bf16x8*)(act + ad[1] + off)};
   }
   __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v) {
-    const bf16x4 hi = __builtin_convertvector(v, bf16x4);
-    const bf16x4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x4), bf16x4);
+    const bf16x4 hi = __builtin_convertvector(v, bf16x4);           // 2 x v_cvt_pk_bf16_f32 (RNE)
+    // hi back to f32 straight from the packed bits (one shift / mask each, no re-conversion)
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 hb = __builtin_bit_cast(u32x2, hi);
+    const f32x4 hf = {__uint_as_float(hb.x << 16), __uint_as_float(hb.x & 0xffff0000u),
+                      __uint_as_float(hb.y << 16), __uint_as_float(hb.y & 0xffff0000u)};
+    const bf16x4 lo = __builtin_convertvector(v - hf, bf16x4);
     *(bf16x4*)(act + ad[0] + off) = hi;
     *(bf16x4*)(act + ad[1] + off) = lo;
   }
@@ -236,16 +241,26 @@ constexpr int IP_MT = 2, IP_NT = 2, IP_NB = 4, IP_BR = WB / IP_NB;
 // from L2 (the four waves of a pair hit the same lines at the same time: mostly L1 hits); the
 // next layer's k-step s is fetched right after its last use in the current layer.
 template <int MODE>
-using LayerA = typename Op<MODE>::A[IP_MT][Op<MODE>::KSTEPS];
+struct LayerA {
+  typename Op<MODE>::A v[IP_MT][Op<MODE>::KSTEPS];
+  f32x4 bias[IP_MT];           // lane quarter q's 4 output channels of each M-tile (accumulator init)
+  __device__ __forceinline__ typename Op<MODE>::A (&operator[](int mm))[Op<MODE>::KSTEPS] { return v[mm]; }
+};
+
+__device__ __forceinline__ f32x4 load_bias(const uint8_t* wl, int m) {
+  return *(const f32x4*)(wl + BIAS_OFF + (16 * m + 4 * ((threadIdx.x & 63) >> 4)) * 4);
+}
 
 template <int MODE>
 __device__ __forceinline__ void load_layer_a(const Tile& tl, int layer, LayerA<MODE>& a) {
   const int mp = (threadIdx.x >> 6) & 1, lane = threadIdx.x & 63;
   const uint8_t* wl = tl.big + (size_t)layer * BIG_BYTES;
 #pragma unroll
-  for (int mm = 0; mm < IP_MT; ++mm)
+  for (int mm = 0; mm < IP_MT; ++mm) {
+    a.bias[mm] = load_bias(wl, IP_MT * mp + mm);
 #pragma unroll
     for (int s = 0; s < Op<MODE>::KSTEPS; ++s) a[mm][s] = Op<MODE>::load_a(wl, IP_MT * mp + mm, s, lane);
+  }
 }
 
 // One Conv1d(64,64,3,d) over the tile, updated in place with a one-block lag.
@@ -255,7 +270,9 @@ __device__ __forceinline__ void load_layer_a(const Tile& tl, int layer, LayerA<M
 // They are then written while block j+1 computes (after its first k-step), so the LDS stores and
 // their epilogue VALU overlap the MFMA stream instead of forming a separate write phase.
 // Sequence: C0 | C1 | S0+C2 | S1+C3 | S2 S3 |.   id[16] = [block][N-tile][M-tile] identities.
-template <int MODE, int EPI, int S>
+// EDGE = false: the tile holds no position outside [0, L) (interior tiles of a spectrum), so the
+// write-back skips the per-row zeroing.
+template <int MODE, int EPI, int S, bool EDGE = true>
 __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], LayerA<MODE>& a, bool has_next) {
   using O = Op<MODE>;
   constexpr int NB = IP_NB, NT = IP_NT, MT = IP_MT, BR = IP_BR;
@@ -264,9 +281,12 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], LayerA<
   const int q = lane >> 4, c16 = lane & 15;
   const uint8_t* wcur = tl.big + (size_t)tl.layer * BIG_BYTES;
   const uint8_t* wnext = wcur + BIG_BYTES;
-  f32x4 bias[MT];
+  // bf16 modes start the accumulators at the folded bias; exact fp32 keeps the reference's
+  // order (sum of products, then + bias) for its 1e-5 parity
+  constexpr bool BIAS_INIT = MODE != MODE_F32;
+  f32x4 bias_l[MT];
 #pragma unroll
-  for (int mm = 0; mm < MT; ++mm) bias[mm] = *(const f32x4*)(wcur + BIAS_OFF + (16 * (MT * mp + mm) + 4 * q) * 4);
+  for (int mm = 0; mm < MT; ++mm) bias_l[mm] = a.bias[mm];
 
   // LDS byte addresses of this lane's B fragments for every k-step (row = first row of the wave's
   // share of block 0), and of its output stores; blocks and N-tiles add multiples of 16 rows,
@@ -290,17 +310,18 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], LayerA<
   f32x4 res[NB][NT][MT];
   auto store_block = [&](int j) {
     const int rb = BR * j + (BR / 4) * nq;            // first row of this wave's share of block j
-    const bool inside = tl.base + rb >= 0 && tl.base + rb + BR / 4 <= tl.L;
+    const bool inside = !EDGE || (tl.base + rb >= 0 && tl.base + rb + BR / 4 <= tl.L);
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
       const int row = rb + 16 * i + c16;
       const bool zero = !inside && !in_range(tl.base + row, tl.L);       // conv zero padding
 #pragma unroll
       for (int mm = 0; mm < MT; ++mm) {
-        f32x4 v = res[j][i][mm] + bias[mm];
+        f32x4 v = res[j][i][mm];
+        if (!BIAS_INIT) v += bias_l[mm];
         if (EPI & ADD_ID) v += id[(j * NT + i) * MT + mm];
         if (EPI & RELU) v = __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
-        if (zero) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};
         if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
 #if defined(RDN_ABLATE_NOSTORE)
         if (v[0] == 123456.f)
@@ -310,6 +331,13 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], LayerA<
     }
   };
 
+  // B fragments are software-pipelined one k-step ahead: the reads for k-step s+1 are issued
+  // before the MFMAs of k-step s, so LDS latency hides under 2 x 3 x 16-cycle MFMA chains; the
+  // first k-step of block j+1 is read before the barrier that ends block j (its rows are not
+  // among those the write-backs around that barrier touch: blocks j-2 and j-1).
+  typename O::B bnext[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) bnext[i] = O::load_b_at(tl.lds, badr[0], (uint32_t)(16 * i) * ROWB_F32);
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     f32x4 part[S][NT][MT];
@@ -318,12 +346,12 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], LayerA<
 #pragma unroll
       for (int i = 0; i < NT; ++i)
 #pragma unroll
-        for (int mm = 0; mm < MT; ++mm) part[k][i][mm] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // B fragments are software-pipelined one k-step ahead: the reads for k-step s+1 are issued
-    // before the MFMAs of k-step s, so LDS latency hides under 2 x 3 x 16-cycle MFMA chains.
-    typename O::B bnext[NT];
+        for (int mm = 0; mm < MT; ++mm)
+          part[k][i][mm] = k == 0 && BIAS_INIT ? a.bias[mm] : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (j == NB - 1 && has_next) {                    // last use of this layer's bias
 #pragma unroll
-    for (int i = 0; i < NT; ++i) bnext[i] = O::load_b_at(tl.lds, badr[0], (uint32_t)(BR * j + 16 * i) * ROWB_F32);
+      for (int mm = 0; mm < MT; ++mm) a.bias[mm] = load_bias(wnext, MT * mp + mm);
+    }
 #pragma unroll
     for (int s = 0; s < O::KSTEPS; ++s) {
       typename O::B bcur[NT];
@@ -369,6 +397,10 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], LayerA<
         for (int k = 1; k < S; ++k) v += part[k][i][mm];
         res[j][i][mm] = v;
       }
+    if (j + 1 < NB) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) bnext[i] = O::load_b_at(tl.lds, badr[0], (uint32_t)(BR * (j + 1) + 16 * i) * ROWB_F32);
+    }
     lds_barrier();                 // every wave is done reading the rows block j needed
   }
   store_block(NB - 2);

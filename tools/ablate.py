@@ -15,8 +15,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fiber-raman-intensity_amd", "csrc")
 OUT = os.path.join(ROOT, "tools", "ablate_build")
-VARIANTS = {"base": "", "legacy16": "-DRDN_BF16_LEGACY", "nolds": "-DRDN_ABLATE_NOLDS", "nomfma": "-DRDN_ABLATE_NOMFMA",
-            "nostore": "-DRDN_ABLATE_NOSTORE", "noaload": "-DRDN_ABLATE_NOALOAD", "pf3": "-DRDN_H16_PF=3", "ieee": ""}
+VARIANTS = {"base": "", "prev": "", "legacy16": "-DRDN_BF16_LEGACY", "nolds": "-DRDN_ABLATE_NOLDS",
+            "nomfma": "-DRDN_ABLATE_NOMFMA", "nostore": "-DRDN_ABLATE_NOSTORE", "noaload": "-DRDN_ABLATE_NOALOAD",
+            "pf3": "-DRDN_H16_PF=3", "ieee": ""}
 
 
 def build():
