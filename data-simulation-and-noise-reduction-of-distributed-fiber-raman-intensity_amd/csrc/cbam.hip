@@ -254,8 +254,12 @@ __global__ __launch_bounds__(THREADS) void segment(const uint8_t* __restrict__ b
     stem<MODE, true>(tl, 0);
     __syncthreads();
   }
-  float v = head<MODE>(tl, sg.head_slot);
-  if (sg.head_sigmoid) v = sigm(v);
+  float v[HEAD_ROWS];
+  head<MODE>(tl, sg.head_slot, v);
+  if (sg.head_sigmoid) {
+#pragma unroll
+    for (int k = 0; k < HEAD_ROWS; ++k) v[k] = sigm(v[k]);
+  }
   store_out(tl, y, n, v, sg.halo, T);
 }
 

@@ -14,75 +14,97 @@ namespace ip {
   template <int MODE, bool EDGE> \
   __device__ __forceinline__ void name##_body(Tile& tl, float* y, int n, int L, int T)
 
+// 128-row blocks per tile: 640-row tiles (the whole LDS, no guard rows) everywhere except DSDN,
+// whose ResidualBlock identity lives in VGPRs (20 vs 16 f32x4 per lane at 640 rows: spills).
+template <int ARCH> struct NetGeo { static constexpr int NBK = 5; };
+template <> struct NetGeo<DSDN> { static constexpr int NBK = 4; };
+
 IP_BODY(denoisecnn) {
+  constexpr int NBK = NetGeo<DENOISECNN>::NBK;
   constexpr int H = fused_halo(DENOISECNN);
   using G = Geo<MODE, false>;
-  f32x4 id[16];
+  f32x4 id[16 * NBK / 4];
   LayerA<MODE> a;
   load_layer_a<MODE>(tl, 0, a);
-  zero_guards(tl.lds);
-  stem<MODE>(tl, 0);
+  if (NBK == 4) zero_guards(tl.lds);
+  stem<MODE, false, NBK>(tl, 0);
   __syncthreads();
-  for (int i = 0; i < 18; ++i) conv<MODE, RELU, G::S, EDGE>(tl, 1, id, a, i + 1 < 18);
-  store_out(tl, y, n, head<MODE>(tl, 1), H, T);
+  for (int i = 0; i < 18; ++i) conv<MODE, RELU, G::S, EDGE, NBK>(tl, 1, id, a, i + 1 < 18);
+  float o[HEAD_ROWS];
+  head<MODE, NBK>(tl, 1, o);
+  store_out(tl, y, n, o, H, T);
 }
 
 IP_BODY(rrcdnet) {
+  constexpr int NBK = NetGeo<RRCDNET>::NBK;
   constexpr int H = fused_halo(RRCDNET);
   using G = Geo<MODE, false>;
-  f32x4 id[16];
+  f32x4 id[16 * NBK / 4];
   LayerA<MODE> a;
   load_layer_a<MODE>(tl, 0, a);
-  zero_guards(tl.lds);
-  stem<MODE>(tl, 0);
+  if (NBK == 4) zero_guards(tl.lds);
+  stem<MODE, false, NBK>(tl, 0);
   __syncthreads();
-  for (int i = 0; i < 15; ++i) conv<MODE, RELU, G::S, EDGE>(tl, 1, id, a, true);
-  const float r = head<MODE>(tl, 2);
+  for (int i = 0; i < 15; ++i) conv<MODE, RELU, G::S, EDGE, NBK>(tl, 1, id, a, true);
+  float r[HEAD_ROWS];
+  head<MODE, NBK>(tl, 2, r);
   __syncthreads();               // the left stem overwrites the rows the right head just read
-  stem<MODE>(tl, 1);
+  stem<MODE, false, NBK>(tl, 1);
   __syncthreads();
-  for (int i = 0; i < 14; ++i) conv<MODE, RELU, G::S, EDGE>(tl, i == 7 ? 1 : 2, id, a, i + 1 < 14);
-  const float l = head<MODE>(tl, 3);
-  const int p = tl.base + (int)threadIdx.x;
-  const float xv = in_range(p, L) ? tl.x[p] : 0.f;
-  store_out(tl, y, n, xv - (r + l) / 2.0f, H, T);
+  for (int i = 0; i < 14; ++i) conv<MODE, RELU, G::S, EDGE, NBK>(tl, i == 7 ? 1 : 2, id, a, i + 1 < 14);
+  float l[HEAD_ROWS];
+  head<MODE, NBK>(tl, 3, l);
+#pragma unroll
+  for (int k = 0; k < HEAD_ROWS; ++k) {
+    const int p = tl.base + (int)threadIdx.x + THREADS * k;
+    const float xv = in_range(p, L) ? tl.x[p] : 0.f;
+    r[k] = xv - (r[k] + l[k]) / 2.0f;
+  }
+  store_out(tl, y, n, r, H, T);
 }
 
 IP_BODY(dsdn) {
+  constexpr int NBK = NetGeo<DSDN>::NBK;
   constexpr int H = fused_halo(DSDN);
   using G = Geo<MODE, true>;
-  f32x4 id[16];
+  f32x4 id[16 * NBK / 4];
   LayerA<MODE> a;
   load_layer_a<MODE>(tl, 0, a);
-  zero_guards(tl.lds);
-  stem<MODE>(tl, 0);
+  if (NBK == 4) zero_guards(tl.lds);
+  stem<MODE, false, NBK>(tl, 0);
   __syncthreads();
-  conv<MODE, RELU, G::S, EDGE>(tl, 1, id, a, true);                        // conv1
-  conv<MODE, RELU | SAVE_ID, G::S, EDGE>(tl, 1, id, a, true);              // conv2 -> first block identity
+  conv<MODE, RELU, G::S, EDGE, NBK>(tl, 1, id, a, true);                        // conv1
+  conv<MODE, RELU | SAVE_ID, G::S, EDGE, NBK>(tl, 1, id, a, true);              // conv2 -> first block identity
   for (int b = 0; b < 15; ++b) {
-    conv<MODE, RELU, G::S, EDGE>(tl, 1, id, a, true);                      // relu(bn1(conv1 x))
-    conv<MODE, RELU | ADD_ID | SAVE_ID, G::S, EDGE>(tl, 1, id, a, b < 14); // relu(bn2(conv2 .) + x)
+    conv<MODE, RELU, G::S, EDGE, NBK>(tl, 1, id, a, true);                      // relu(bn1(conv1 x))
+    conv<MODE, RELU | ADD_ID | SAVE_ID, G::S, EDGE, NBK>(tl, 1, id, a, b < 14); // relu(bn2(conv2 .) + x)
   }
-  store_out(tl, y, n, head<MODE>(tl, 1), H, T);
+  float o[HEAD_ROWS];
+  head<MODE, NBK>(tl, 1, o);
+  store_out(tl, y, n, o, H, T);
 }
 
 IP_BODY(pidn) {
+  constexpr int NBK = NetGeo<PIDN>::NBK;
   constexpr int H = fused_halo(PIDN);
   using G = Geo<MODE, false>;
-  f32x4 id[16];
+  f32x4 id[16 * NBK / 4];
   LayerA<MODE> a;
   load_layer_a<MODE>(tl, 0, a);
-  zero_guards(tl.lds);
-  stem<MODE>(tl, 0);
+  if (NBK == 4) zero_guards(tl.lds);
+  stem<MODE, false, NBK>(tl, 0);
   __syncthreads();
   for (int b = 0; b < 15; ++b) {
-    conv<MODE, RELU, G::S, EDGE>(tl, 1, id, a, true);
-    conv<MODE, 0, G::S, EDGE>(tl, 1, id, a, b < 14);
+    conv<MODE, RELU, G::S, EDGE, NBK>(tl, 1, id, a, true);
+    conv<MODE, 0, G::S, EDGE, NBK>(tl, 1, id, a, b < 14);
   }
-  stem<MODE, true>(tl, 0);       // + identity (the stem output), recomputed from x
+  stem<MODE, true, NBK>(tl, 0);       // + identity (the stem output), recomputed from x
   __syncthreads();
-  const float v = head<MODE>(tl, 1);
-  store_out(tl, y, n, 1.0f / (1.0f + expf(-v)), H, T);
+  float o[HEAD_ROWS];
+  head<MODE, NBK>(tl, 1, o);
+#pragma unroll
+  for (int k = 0; k < HEAD_ROWS; ++k) o[k] = 1.0f / (1.0f + expf(-o[k]));
+  store_out(tl, y, n, o, H, T);
 }
 
 #define IP_KERNEL(name, arch)                                                                              \
@@ -92,7 +114,7 @@ IP_BODY(pidn) {
     extern __shared__ __attribute__((aligned(16))) char lds[];                                             \
     int n;                                                                                                 \
     Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(arch), n);                                   \
-    if (tl.base >= 0 && tl.base + WB <= L) name##_body<MODE, false>(tl, y, n, L, T);                       \
+    if (tl.base >= 0 && tl.base + TileGeo<NetGeo<arch>::NBK>::WB <= L) name##_body<MODE, false>(tl, y, n, L, T); \
     else name##_body<MODE, true>(tl, y, n, L, T);                                                          \
   }
 
@@ -117,17 +139,20 @@ hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const 
     case PIDN: k = x3 ? ip::pidn<ip::MODE_X3> : ip::pidn<ip::MODE_F32>; break;
     default: return hipErrorInvalidValue;
   }
+  const int nbk = arch == DSDN ? ip::NetGeo<DSDN>::NBK : ip::NetGeo<RRCDNET>::NBK;
+  const int wb = 128 * nbk;
+  const uint32_t lds = nbk == 4 ? ip::TileGeo<4>::LDS : ip::TileGeo<5>::LDS;
   static bool attr_set[2][8] = {};
   if (!attr_set[x3][arch]) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ip::LDS_BYTES);
+    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr_set[x3][arch] = true;
   }
-  const int H = fused_halo(arch), T = WB - 2 * H, tiles = (L + T - 1) / T;
+  const int H = fused_halo(arch), T = wb - 2 * H, tiles = (L + T - 1) / T;
   const int64_t chunk = (int64_t)(0x7fffffff / tiles);
   for (int64_t n0 = 0; n0 < n; n0 += chunk) {
     const int64_t nn = n - n0 < chunk ? n - n0 : chunk;
-    hipLaunchKernelGGL(k, dim3((unsigned)(nn * tiles)), dim3(THREADS), ip::LDS_BYTES, stream, blob, x + n0 * L,
+    hipLaunchKernelGGL(k, dim3((unsigned)(nn * tiles)), dim3(THREADS), lds, stream, blob, x + n0 * L,
                        y + n0 * L, L, T, tiles);
   }
   return hipGetLastError();

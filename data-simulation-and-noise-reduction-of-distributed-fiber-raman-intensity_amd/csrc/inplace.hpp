@@ -24,7 +24,23 @@ namespace rdn {
 namespace ip {
 
 constexpr int MODE_F32 = 0, MODE_B1 = 1, MODE_X3 = 2;
-constexpr uint32_t LDS_BYTES = ACT_BYTES_F32;                    // 132096
+constexpr uint32_t LDS_BYTES = ACT_BYTES_F32;                    // 132096 (512 rows + guards)
+
+// Tile geometry by number of 128-row blocks: NBK = 4 -> 512 rows with 2 zero guard rows per side
+// (the CBAM segment kernels, which keep scratch behind the buffer); NBK = 5 -> 640 rows, no guard
+// rows, the whole 160 KiB LDS (fused_inplace.hip).  Without guards a tap that leaves the tile
+// wraps to its other end: those rows are outside every output's receptive field (the halo covers
+// the stack's depth), so any finite value serves; spectrum positions outside [0, L) are re-zeroed
+// by the write-backs of edge tiles.
+template <int NBK> struct TileGeo {
+  static constexpr int WB = 128 * NBK;
+  static constexpr bool WRAP = NBK != 4;
+  static constexpr int GRD = WRAP ? 0 : GUARD;
+  static constexpr uint32_t LDS = (WB + 2 * GRD) * ROWB_F32;
+  __device__ static int row(int r) { return WRAP ? (r < 0 ? r + WB : (r >= WB ? r - WB : r)) : r + GRD; }
+};
+static_assert(TileGeo<4>::LDS == LDS_BYTES, "CBAM geometry");
+static_assert(TileGeo<5>::LDS == 163840, "fused geometry fills the LDS");
 constexpr int BIG_BYTES = BIG_BYTES_F32;                         // both modes: 49408 B per layer
 constexpr int BIAS_OFF = BIG_FRAG_FLOATS_F32 * 4;                // 49152
 
@@ -180,10 +196,12 @@ __device__ __forceinline__ const cfloat* small_slot(const Tile& tl, int slot) {
 
 // Conv1d(1, 64, 3, padding=1) (+ folded BN) + ReLU, one row per thread, fp32; ACCUM adds the
 // result onto the resident row (PIDN/train.py:105, identity recomputed from x).
-template <int MODE, bool ACCUM = false>
+template <int MODE, bool ACCUM = false, int NBK = 4>
 __device__ __forceinline__ void stem(const Tile& tl, int slot) {
+  using TG = TileGeo<NBK>;
   const cfloat* sw = small_slot(tl, slot);
-  const int j = threadIdx.x;
+  for (int j = threadIdx.x; j < TG::WB; j += THREADS) {
+  const int pr = TG::row(j);
   const int p = tl.base + j;
   const float xm = in_range(p - 1, tl.L) ? tl.x[p - 1] : 0.f;
   const float x0 = in_range(p, tl.L) ? tl.x[p] : 0.f;
@@ -191,7 +209,7 @@ __device__ __forceinline__ void stem(const Tile& tl, int slot) {
   const bool valid = in_range(p, tl.L);
 #pragma unroll
   for (int cb = 0; cb < 16; ++cb) {
-    f32x4 v = ACCUM ? Op<MODE>::load4(tl.lds, j + GUARD, 4 * cb) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 v = ACCUM ? Op<MODE>::load4(tl.lds, pr, 4 * cb) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int c = cb * 4 + i;
@@ -203,19 +221,28 @@ __device__ __forceinline__ void stem(const Tile& tl, int slot) {
       if (ACCUM) a += v[i];
       v[i] = valid ? a : 0.f;
     }
-    Op<MODE>::store4(tl.lds, j + GUARD, 4 * cb, v);
+    Op<MODE>::store4(tl.lds, pr, 4 * cb, v);
+  }
   }
 }
 
-// Conv1d(64, 1, 3, padding=1), one row per thread, fp32 weights and accumulate.
-template <int MODE>
-__device__ __forceinline__ float head(const Tile& tl, int slot) {
+// Conv1d(64, 1, 3, padding=1), one row per thread (row j = threadIdx.x + THREADS * k in out[k]),
+// fp32 weights and accumulate.
+constexpr int HEAD_ROWS = 2;      // rows per thread: ceil(640 / 512)
+template <int MODE, int NBK = 4>
+__device__ __forceinline__ void head(const Tile& tl, int slot, float (&out)[HEAD_ROWS]) {
+  using TG = TileGeo<NBK>;
+  static_assert(TG::WB <= HEAD_ROWS * THREADS, "head rows per thread");
   const cfloat* hw = small_slot(tl, slot);
-  const int j = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < HEAD_ROWS; ++k) {
+  const int j = threadIdx.x + THREADS * k;
+  out[k] = 0.f;
+  if (j >= TG::WB) continue;
   float a = hw[192];
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
-    const int prow = j + GUARD + t - 1;
+    const int prow = TG::row(j + t - 1);
 #pragma unroll 4
     for (int cb = 0; cb < 16; ++cb) {
       const f32x4 v = Op<MODE>::load4(tl.lds, prow, 4 * cb);
@@ -223,7 +250,8 @@ __device__ __forceinline__ float head(const Tile& tl, int slot) {
       for (int i = 0; i < 4; ++i) a = fmaf(hw[3 * (cb * 4 + i) + t], v[i], a);
     }
   }
-  return a;
+  out[k] = a;
+  }
 }
 
 // LDS-only workgroup barrier: waits for this wave's LDS traffic, NOT for its outstanding global
@@ -272,10 +300,12 @@ __device__ __forceinline__ void load_layer_a(const Tile& tl, int layer, LayerA<M
 // Sequence: C0 | C1 | S0+C2 | S1+C3 | S2 S3 |.   id[16] = [block][N-tile][M-tile] identities.
 // EDGE = false: the tile holds no position outside [0, L) (interior tiles of a spectrum), so the
 // write-back skips the per-row zeroing.
-template <int MODE, int EPI, int S, bool EDGE = true>
-__device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], LayerA<MODE>& a, bool has_next) {
+template <int MODE, int EPI, int S, bool EDGE = true, int NBK = 4>
+__device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4], LayerA<MODE>& a, bool has_next) {
   using O = Op<MODE>;
-  constexpr int NB = IP_NB, NT = IP_NT, MT = IP_MT, BR = IP_BR;
+  using TG = TileGeo<NBK>;
+  constexpr int NB = NBK, NT = IP_NT, MT = IP_MT, BR = IP_BR;
+  constexpr int TS = O::KSTEPS / 3;                  // k-steps per tap
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int mp = w & 1, nq = w >> 1;
   const int q = lane >> 4, c16 = lane & 15;
@@ -292,13 +322,31 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], LayerA<
   // share of block 0), and of its output stores; blocks and N-tiles add multiples of 16 rows,
   // which leave the row swizzle unchanged (-> ds_* immediate offsets).
   uint32_t badr[O::KSTEPS][O::PLANES], sadr[MT][O::PLANES];
-  const int prow0 = GUARD + (BR / 4) * nq + c16;
+  const int prow0 = TG::GRD + (BR / 4) * nq + c16;
 #pragma unroll
   for (int s = 0; s < O::KSTEPS; ++s) {
-    const int pr = prow0 + (O::tap(s) - 1) * dil;
+    const int pr = prow0 + (O::tap(s) - 1) * dil;  // < 0 (wave 0, tap 0) only in WRAP geometry: block 0 uses bfirst
 #pragma unroll
     for (int p = 0; p < O::PLANES; ++p) badr[s][p] = pr * ROWB_F32 + ((O::bslot(s, q, p) ^ swz256(pr)) << 4);
   }
+  // WRAP: the taps that can leave the tile -- tap 0 of block 0, N-tile 0 (waves nq = 0) and tap 2 of
+  // the last block, last N-tile (nq = 3) -- read through wrapped absolute addresses
+  uint32_t bfirst[TS][O::PLANES], blast[TS][O::PLANES];
+  if (TG::WRAP) {
+    const int pf = TG::row(prow0 - dil), pl = TG::row(prow0 + BR * (NB - 1) + 16 * (NT - 1) + dil);
+#pragma unroll
+    for (int s = 0; s < TS; ++s)
+#pragma unroll
+      for (int p = 0; p < O::PLANES; ++p) {
+        bfirst[s][p] = pf * ROWB_F32 + ((O::bslot(s, q, p) ^ swz256(pf)) << 4);
+        blast[s][p] = pl * ROWB_F32 + ((O::bslot(2 * TS + s, q, p) ^ swz256(pl)) << 4);
+      }
+  }
+  auto read_b = [&](int j, int s, int i) -> typename O::B {
+    if (TG::WRAP && j == 0 && s < TS && i == 0) return O::load_b_at(tl.lds, bfirst[s], 0);
+    if (TG::WRAP && j == NB - 1 && s >= 2 * TS && i == NT - 1) return O::load_b_at(tl.lds, blast[s - 2 * TS], 0);
+    return O::load_b_at(tl.lds, badr[s], (uint32_t)(BR * j + 16 * i) * ROWB_F32);
+  };
 #pragma unroll
   for (int mm = 0; mm < MT; ++mm)
 #pragma unroll
@@ -337,7 +385,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], LayerA<
   // among those the write-backs around that barrier touch: blocks j-2 and j-1).
   typename O::B bnext[NT];
 #pragma unroll
-  for (int i = 0; i < NT; ++i) bnext[i] = O::load_b_at(tl.lds, badr[0], (uint32_t)(16 * i) * ROWB_F32);
+  for (int i = 0; i < NT; ++i) bnext[i] = read_b(0, 0, i);
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     f32x4 part[S][NT][MT];
@@ -364,7 +412,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], LayerA<
           bnext[i] = bcur[i];
           asm volatile("" : "+v"(reinterpret_cast<f32x4&>(bnext[i])) ::);
 #else
-          bnext[i] = O::load_b_at(tl.lds, badr[s + 1], (uint32_t)(BR * j + 16 * i) * ROWB_F32);
+          bnext[i] = read_b(j, s + 1, i);
 #endif
         }
       }
@@ -399,7 +447,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16], LayerA<
       }
     if (j + 1 < NB) {
 #pragma unroll
-      for (int i = 0; i < NT; ++i) bnext[i] = O::load_b_at(tl.lds, badr[0], (uint32_t)(BR * (j + 1) + 16 * i) * ROWB_F32);
+      for (int i = 0; i < NT; ++i) bnext[i] = read_b(j + 1, 0, i);
     }
     lds_barrier();                 // every wave is done reading the rows block j needed
   }
@@ -430,10 +478,13 @@ __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const 
   return tl;
 }
 
-__device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, float v, int halo, int T) {
-  const int j = threadIdx.x;
-  const int p = tl.base + j;
-  if (j >= halo && j < halo + T && p < tl.L) y[(size_t)n * tl.L + p] = v;
+__device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, const float (&v)[HEAD_ROWS], int halo, int T) {
+#pragma unroll
+  for (int k = 0; k < HEAD_ROWS; ++k) {
+    const int j = threadIdx.x + THREADS * k;
+    const int p = tl.base + j;
+    if (j >= halo && j < halo + T && p < tl.L) y[(size_t)n * tl.L + p] = v[k];
+  }
 }
 
 }  // namespace ip
