@@ -24,6 +24,9 @@ namespace rdn {
 namespace ip {
 
 constexpr int MODE_F32 = 0, MODE_B1 = 1, MODE_X3 = 2;
+#ifndef RDN_IP_SPREAD_STORE
+#define RDN_IP_SPREAD_STORE 1
+#endif
 constexpr uint32_t LDS_BYTES = ACT_BYTES_F32;                    // 132096 (512 rows + guards)
 
 // Tile geometry by number of 128-row blocks: NBK = 4 -> 512 rows with 2 zero guard rows per side
@@ -356,27 +359,28 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
     }
 
   f32x4 res[NB][NT][MT];
-  auto store_block = [&](int j) {
+  // write-back of N-tile i, M-tile mm of block j (bias / identity, ReLU, zero padding, round)
+  auto store_piece = [&](int j, int i, int mm) {
     const int rb = BR * j + (BR / 4) * nq;            // first row of this wave's share of block j
     const bool inside = !EDGE || (tl.base + rb >= 0 && tl.base + rb + BR / 4 <= tl.L);
-#pragma unroll
-    for (int i = 0; i < NT; ++i) {
-      const int row = rb + 16 * i + c16;
-      const bool zero = !inside && !in_range(tl.base + row, tl.L);       // conv zero padding
-#pragma unroll
-      for (int mm = 0; mm < MT; ++mm) {
-        f32x4 v = res[j][i][mm];
-        if (!BIAS_INIT) v += bias_l[mm];
-        if (EPI & ADD_ID) v += id[(j * NT + i) * MT + mm];
-        if (EPI & RELU) v = __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
-        if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
+    const int row = rb + 16 * i + c16;
+    const bool zero = !inside && !in_range(tl.base + row, tl.L);         // conv zero padding
+    f32x4 v = res[j][i][mm];
+    if (!BIAS_INIT) v += bias_l[mm];
+    if (EPI & ADD_ID) v += id[(j * NT + i) * MT + mm];
+    if (EPI & RELU) v = __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
+    if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
 #if defined(RDN_ABLATE_NOSTORE)
-        if (v[0] == 123456.f)
+    if (v[0] == 123456.f)
 #endif
-        O::store4_at(tl.lds, sadr[mm], (uint32_t)(BR * j + 16 * i) * ROWB_F32, v);
-      }
-    }
+    O::store4_at(tl.lds, sadr[mm], (uint32_t)(BR * j + 16 * i) * ROWB_F32, v);
+  };
+  auto store_block = [&](int j) {
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int mm = 0; mm < MT; ++mm) store_piece(j, i, mm);
   };
 
   // B fragments are software-pipelined one k-step ahead: the reads for k-step s+1 are issued
@@ -432,7 +436,13 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #pragma unroll
         for (int mm = 0; mm < MT; ++mm) a[mm][s] = O::load_a(wnext, MT * mp + mm, s, lane);
       }
+#if RDN_IP_SPREAD_STORE
+      // lagged write-back of block j-2, one (N-tile, M-tile) piece per k-step: the LDS write
+      // bursts of the 8 waves spread over the block instead of landing on its first k-step
+      if (j >= 2 && s < NT * MT) store_piece(j - 2, s / MT, s % MT);
+#else
       if (s == 0 && j >= 2) store_block(j - 2);                        // lagged write-back
+#endif
       // keep B-fragment reads within their k-step (VGPR budget of 2 waves/SIMD)
       __builtin_amdgcn_sched_barrier(0);
     }

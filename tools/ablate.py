@@ -17,7 +17,8 @@ CSRC = os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fi
 OUT = os.path.join(ROOT, "tools", "ablate_build")
 VARIANTS = {"base": "", "prev": "", "legacy16": "-DRDN_BF16_LEGACY", "nolds": "-DRDN_ABLATE_NOLDS",
             "nomfma": "-DRDN_ABLATE_NOMFMA", "nostore": "-DRDN_ABLATE_NOSTORE", "noaload": "-DRDN_ABLATE_NOALOAD",
-            "pf3": "-DRDN_H16_PF=3", "ieee": ""}
+            "pf3": "-DRDN_H16_PF=3", "ieee": "", "nospread": "-DRDN_IP_SPREAD_STORE=0", "prio": "-DRDN_IP_PRIO=1",
+            "prionospread": "-DRDN_IP_PRIO=1 -DRDN_IP_SPREAD_STORE=0"}
 
 
 def build():
