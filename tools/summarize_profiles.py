@@ -1,0 +1,76 @@
+"""Summarise a scripts/gpu_profile.sh run into the committed evidence under profiles/.
+
+    python tools/summarize_profiles.py gpurun_out/prof profiles/r01
+
+Writes <dst>/rocprof/kernel_stats_bench.csv (rocprofv3 --kernel-trace --stats of the default
+`python bench.py`), <dst>/rocprof/pmc_summary.json (per-dispatch averages of every PMC counter for
+the fused RRCDNet kernels), <dst>/parity_table.md, and profiles/traffic.json: HBM bytes per
+spectrum of each dtype's kernel = (2 x FETCH_SIZE + WRITE_SIZE) KiB per dispatch / batch — FETCH_SIZE
+doubled per the gfx950 correction of MI355X_MICROARCH.md §HBM (it reports half the bytes of wide
+streaming reads).
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+KERNELS = {"bf16x3": "rdn::ip::rrcdnet<2>", "bf16": "rdn::h16::rrcdnet"}
+BATCH = 8192          # bench.py default --batch (the PMC passes run the default batch)
+
+
+def counters(path, kernel):
+    """{counter: mean per dispatch} over the dispatches of `kernel` in one PMC pass directory."""
+    sums, counts = {}, {}
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if kernel not in r["Kernel_Name"]:
+                    continue
+                key = (r["Counter_Name"], r.get("Dispatch_Id"))
+                sums[key] = sums.get(key, 0.0) + float(r["Counter_Value"])
+    per = {}
+    for (name, _), v in sums.items():
+        per.setdefault(name, []).append(v)
+    return {k: sum(v) / len(v) for k, v in per.items()}
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    os.makedirs(os.path.join(dst, "rocprof"), exist_ok=True)
+    stats = glob.glob(os.path.join(src, "kt", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(dst, "rocprof", "kernel_stats_bench.csv"))
+    if os.path.exists(os.path.join(src, "parity.md")):
+        shutil.copy(os.path.join(src, "parity.md"), os.path.join(dst, "parity_table.md"))
+    summary, traffic = {}, {}
+    for dt, kern in KERNELS.items():
+        c = {}
+        for d in sorted(glob.glob(os.path.join(src, f"pmc_{dt}_*"))):
+            if os.path.isdir(d):
+                c.update(counters(d, kern))
+        if not c:
+            continue
+        summary[f"RRCDNet/{dt}"] = {"kernel": kern, "batch": BATCH, "per_dispatch": c}
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            kib = 2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]
+            traffic[f"RRCDNet/{dt}"] = {
+                "bytes_per_spectrum": kib * 1024 / BATCH,
+                "source": f"{dst}/rocprof/pmc_summary.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+                          f"{kern}, batch {BATCH}, (2*FETCH_SIZE+WRITE_SIZE) KiB per dispatch / {BATCH}"}
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "SQ_BUSY_CU_CYCLES" in c:
+            summary[f"RRCDNet/{dt}"]["mfma_busy_frac_of_simd_cycles"] = (
+                c["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * c["SQ_BUSY_CU_CYCLES"]))
+    with open(os.path.join(dst, "rocprof", "pmc_summary.json"), "w") as fh:
+        json.dump(summary, fh, indent=1)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if traffic:
+        with open(os.path.join(root, "profiles", "traffic.json"), "w") as fh:
+            json.dump(traffic, fh, indent=1)
+    print(json.dumps({"traffic": traffic, "mfma_busy": {k: v.get("mfma_busy_frac_of_simd_cycles") for k, v in summary.items()}},
+                     indent=1))
+
+
+if __name__ == "__main__":
+    main()
