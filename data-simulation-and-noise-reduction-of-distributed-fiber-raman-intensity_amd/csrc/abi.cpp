@@ -12,7 +12,6 @@
 namespace rdn {
 std::string pack(int arch, int dtype, const float* const* tensors, const int64_t* numels, int n, void* dst, size_t cap);
 size_t packed_bytes(const std::vector<Op>& spec, int dtype);
-hipError_t launch_fused_bf16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
 hipError_t launch_fused16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
 hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                 hipStream_t s);
@@ -125,11 +124,7 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
       return fail(RDN_ESIZE, "rdn_forward: workspace too small, need " + std::to_string(need) + " bytes");
     return hip_check(rdn::launch_cbam_forward(arch, dtype, blob, x, y, n, (int)L, ws, ws_bytes, s), "cbam forward");
   }
-#if defined(RDN_BF16_LEGACY)
-  if (dtype == RDN_BF16) return hip_check(rdn::launch_fused_bf16(arch, blob, x, y, n, (int)L, s), "fused bf16 forward");
-#else
   if (dtype == RDN_BF16) return hip_check(rdn::launch_fused16(arch, blob, x, y, n, (int)L, s), "fused bf16 forward");
-#endif
   return hip_check(rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, s), "fused in-place forward");
   RDN_GUARD_END
 }

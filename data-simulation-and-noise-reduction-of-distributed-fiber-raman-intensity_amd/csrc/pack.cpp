@@ -121,8 +121,8 @@ std::vector<std::string> param_names(const std::vector<Op>& spec) {
   return out;
 }
 
-// Weight layout of the big section: the fused bf16 kernels (non-CBAM networks, bf16) keep the
-// head as an MFMA layer (M-row 0) in 24832-byte layers; every other (network, dtype) runs on the
+// Weight layout of the big section: the fused bf16 kernels (fused16.hip: non-CBAM networks, bf16)
+// keep the head as an MFMA layer (M-row 0) in 24832-byte layers, K order permuted (h16_channel); every other (network, dtype) runs on the
 // in-place 256-byte-row engine: f32 fragments, or bf16 hi/lo fragments (bf16 uses only hi).
 static bool has_cbam(const std::vector<Op>& spec) {
   for (const Op& o : spec)
@@ -203,11 +203,7 @@ static void pack_big_bf16(const Folded& f, uint8_t* dst) {
       for (int lane = 0; lane < 64; ++lane)
         for (int j = 0; j < 8; ++j) {
           const int t = s >> 1, u = s & 1;
-#if defined(RDN_BF16_LEGACY)
-          const int co = 16 * m + (lane & 15), ci = 32 * u + 8 * (lane >> 4) + j;
-#else
           const int co = 16 * m + (lane & 15), ci = h16_channel(4 * u + (lane >> 4), j);
-#endif
           const double v = co < f.cout ? f.W(co, ci, t) : 0.0;
           frag[(((m * 6 + s) * 64) + lane) * 8 + j] = to_bf16(v);
         }

@@ -15,7 +15,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fiber-raman-intensity_amd", "csrc")
 OUT = os.path.join(ROOT, "tools", "ablate_build")
-VARIANTS = {"base": "", "prev": "", "legacy16": "-DRDN_BF16_LEGACY", "nolds": "-DRDN_ABLATE_NOLDS",
+VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "nomfma": "-DRDN_ABLATE_NOMFMA", "nostore": "-DRDN_ABLATE_NOSTORE", "noaload": "-DRDN_ABLATE_NOALOAD",
             "pf3": "-DRDN_H16_PF=3", "ieee": "", "nospread": "-DRDN_IP_SPREAD_STORE=0", "prio": "-DRDN_IP_PRIO=1",
             "prionospread": "-DRDN_IP_PRIO=1 -DRDN_IP_SPREAD_STORE=0"}
@@ -25,7 +25,7 @@ def build():
     import torch
     tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
     os.makedirs(OUT, exist_ok=True)
-    srcs = ["fused16.hip", "fused_bf16.hip", "fused_inplace.hip", "cbam.hip", "generator.hip", "metrics.hip", "abi.cpp",
+    srcs = ["fused16.hip", "fused_inplace.hip", "cbam.hip", "generator.hip", "metrics.hip", "abi.cpp",
             "pack.cpp"]
     only = sys.argv[2:]
     for name, flag in VARIANTS.items():
@@ -36,7 +36,7 @@ def build():
             o = os.path.join(OUT, f"{name}_{s}.o")
             cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mcode-object-version=5",
                    "-fno-gpu-rdc", "-c", os.path.join(CSRC, s), "-o", o] + flag.split()
-            if s in ("fused16.hip", "fused_bf16.hip", "fused_inplace.hip", "cbam.hip") and name != "ieee":
+            if s in ("fused16.hip", "fused_inplace.hip", "cbam.hip") and name != "ieee":
                 cmd += ["-fno-honor-nans", "-mno-amdgpu-ieee"]
             if s == "generator.hip":
                 cmd += ["-ffp-contract=off"]
