@@ -15,6 +15,7 @@
 //             sum (fp64) and max of u over the tile's own positions for the next CBAM; or, for
 //             the last segment, runs the head (ADSDN: conv_out; APIDN: sigmoid(conv_out(h + h0))).
 // Intermediates live in HBM as fp32 [n][L][64] (256 B per position).
+#include <cstdlib>
 #include <vector>
 
 #include "inplace.hpp"
@@ -263,6 +264,311 @@ __global__ __launch_bounds__(THREADS) void segment(const uint8_t* __restrict__ b
   store_out(tl, y, n, v, sg.halo, T);
 }
 
+
+// ---- team-persistent forward ---------------------------------------------------------------------
+//
+// The whole network in ONE launch.  The grid is `teams` x TT co-resident workgroups (one per CU:
+// the tile takes 143 KB of LDS); the TT workgroups of a team own the TT tiles of one spectrum and
+// walk the spectra team, team + teams, ...  Each keeps its tile (512 rows + the whole network's
+// halo, so no halo exchange is needed) in LDS from the stem to the head.  CBAM is pointwise except
+// the +-3-row spatial conv (inside the halo) and the channel pool over the whole spectrum: at each
+// CBAM every tile publishes the per-channel sum (fp64) and max of u over its own positions to a
+// slot, the team meets at a counter, and every tile reduces the TT slots in tile order (so the
+// result is deterministic) into ca.  Hand-off per MI355X_MICROARCH.md §Workgroup dispatch (first
+// row of the sc1 table): slots written with sc1 stores by wave 0, `s_waitcnt vmcnt(0)`, one agent
+// atomic add by lane 0; lane 0 polls the counter with sc1 loads, a workgroup barrier, then sc1 loads
+// of the slots.  The ResidualBlock identity (the block input, all tile rows) is parked in a
+// per-workgroup fp32 buffer in memory (sc1 stores / loads: written and read back by the same CU).
+// A wait that exceeds SPIN_LIMIT polls raises the error word and falls through instead of hanging.
+
+constexpr int SLOT_BYTES = 64 * 8 + 64 * 4;        // per-tile stats: 64 fp64 sums, 64 ordered u32 maxima
+constexpr unsigned SPIN_LIMIT = 1u << 22;          // ~0.3 s of s_sleep polls
+constexpr int TEAM_CTR_STRIDE = 16;                // u32s between team counters (64 B)
+
+struct TeamArgs {
+  int TT;               // workgroups (tiles) per team
+  int teams;
+  int T;                // output positions per tile
+  int halo;
+  int64_t n;            // spectra
+  char* slots;          // [teams][2][TT][SLOT_BYTES]
+  unsigned* counters;   // [teams][TEAM_CTR_STRIDE], zeroed before the launch
+  char* hsave;          // [teams * TT][WB][64] f32
+  unsigned* err;
+};
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// sc1 (L1-bypassing) 16-B access to this workgroup's identity buffer
+__device__ __forceinline__ void hs_store(__amdgpu_buffer_rsrc_t r, int off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);
+}
+__device__ __forceinline__ f32x4 hs_load(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+
+// block input x (all WB tile rows) -> identity buffer
+template <int MODE>
+__device__ void save_identity(const Tile& tl, __amdgpu_buffer_rsrc_t hs) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, sub = lane & 15, rgrp = lane >> 4;
+  for (int r = w * 4 + rgrp; r < WB; r += WAVES * 4) hs_store(hs, (r * 64 + 4 * sub) * 4, Op<MODE>::load4(tl.lds, r + GUARD, 4 * sub));
+}
+
+// per-channel sum / max of u over the tile's own positions -> slot (sc1); arrive at the counter
+template <int MODE>
+__device__ void publish_stats(const Tile& tl, const TeamArgs& ta, char* slot, unsigned* ctr) {
+  char* lds = tl.lds;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, sub = lane & 15, rgrp = lane >> 4;
+  const int H = ta.halo, T = ta.T;
+  double sm[4] = {0, 0, 0, 0};
+  float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int r = H + w * 4 + rgrp; r < H + T; r += WAVES * 4) {
+    if (tl.base + r >= tl.L) break;
+    const f32x4 u = Op<MODE>::load4(lds, r + GUARD, 4 * sub);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      sm[i] += (double)u[i];
+      mx[i] = fmaxf(mx[i], u[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    for (int o = 16; o < 64; o <<= 1) {
+      sm[i] += __shfl_xor(sm[i], o);
+      mx[i] = fmaxf(mx[i], __shfl_xor(mx[i], o));
+    }
+  }
+  double* rs = (double*)(lds + RED_OFF);
+  unsigned* rm = (unsigned*)(lds + RED_OFF + 8 * 64 * 8);
+  if (rgrp == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      rs[w * 64 + 4 * sub + i] = sm[i];
+      rm[w * 64 + 4 * sub + i] = f2ord(mx[i]);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c = threadIdx.x;
+    double s = 0.0;
+    unsigned m = 0;
+    for (int k = 0; k < WAVES; ++k) {
+      s += rs[k * 64 + c];
+      m = max(m, rm[k * 64 + c]);
+    }
+    __hip_atomic_store((double*)slot + c, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((unsigned*)(slot + 512) + c, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every lane's slot stores have landed
+    if (c == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// the team has arrived at `target`: lane 0 polls (sc1), the workgroup barrier releases the rest
+__device__ void team_wait(const TeamArgs& ta, unsigned* ctr, unsigned target) {
+  if (threadIdx.x == 0) {
+    unsigned it = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(8);
+      if (++it > SPIN_LIMIT) {
+        __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Apply a CBAM whose statistics sit in the team's slots (`slots0`: TT slots of this barrier) to u
+// in the tile: h = [identity +] u*ca*sa [then ReLU] (ADSDN/train.py:113-116,143-147;
+// APIDN/train.py:113-116,154-156), written over u.
+constexpr int ID_ITERS = WB / (WAVES * 4);          // rows per thread in the pointwise pass (16)
+constexpr int ID_GROUP = 4;                          // identity loads in flight per thread
+
+template <int MODE>
+__device__ void apply_cbam(const Tile& tl, const TeamArgs& ta, const char* slots0, int cbam_slot, bool bias, int res,
+                           __amdgpu_buffer_rsrc_t hs) {
+  char* lds = tl.lds;
+  float* s1 = (float*)(lds + S1_OFF) + 3;       // index -3 .. 514
+  float* s2 = (float*)(lds + S2_OFF) + 3;
+  float* sa = (float*)(lds + SA_OFF);
+  float* ca = (float*)(lds + CA_OFF);
+  float* h1 = (float*)(lds + H1_OFF);
+  double* red = (double*)(lds + RED_OFF);        // pooled avg / max per channel (2 x 64)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* cw = tl.small + cbam_slot * SMALL_SLOT_FLOATS;      // fc.0.weight [4][64]
+  const float* cw2 = cw + SMALL_SLOT_FLOATS;                       // fc.2.weight [64][4]
+  const float* cmisc = cw2 + SMALL_SLOT_FLOATS;                    // fc.0.bias[4], fc.2.bias[64], sa.w[2][7], sa.b
+
+  // -- the spectrum's per-channel mean and max: reduce the TT slots in tile order
+  if (tid < 64) {
+    double s = 0.0;
+    unsigned m = 0;
+    for (int t = 0; t < ta.TT; ++t) {
+      const char* sl = slots0 + (size_t)t * SLOT_BYTES;
+      s += __hip_atomic_load((const double*)sl + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      m = max(m, __hip_atomic_load((const unsigned*)(sl + 512) + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    red[tid] = (double)(float)(s / (double)tl.L);
+    red[64 + tid] = (double)ord2f(m);
+  }
+  __syncthreads();
+  // -- channel attention: hidden units of the shared MLP for the avg- and max-pooled vectors
+  if (tid < 8) {
+    const int j = tid & 3, which = tid >> 2;        // which: 0 = avg, 1 = max
+    float a = bias ? cmisc[j] : 0.f;
+    for (int c = 0; c < 64; ++c) a = fmaf(cw[j * 64 + c], (float)red[which * 64 + c], a);
+    h1[tid] = fmaxf(a, 0.f);
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float oa = bias ? cmisc[4 + tid] : 0.f, om = oa;
+    for (int j = 0; j < 4; ++j) {
+      oa = fmaf(cw2[tid * 4 + j], h1[j], oa);
+      om = fmaf(cw2[tid * 4 + j], h1[4 + j], om);
+    }
+    ca[tid] = sigm(oa + om);
+  }
+  __syncthreads();
+
+  // -- spatial statistics of u*ca per tile row (rows beyond the tile: 0; they feed only halo rows)
+  const int sub = lane & 15, rgrp = lane >> 4;
+  const f32x4 cav = *(const f32x4*)(ca + 4 * sub);
+  for (int r = w * 4 + rgrp - 3; r < WB + 3; r += WAVES * 4) {
+    const int p = tl.base + r;
+    const bool in = p >= 0 && p < tl.L && r >= 0 && r < WB;   // conv7 zero-pads the [mean; max] map
+    float sm = 0.f, mx = -INFINITY;
+    if (in) {
+      const f32x4 u = Op<MODE>::load4(lds, r + GUARD, 4 * sub);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = u[i] * cav[i];
+        sm += v;
+        mx = fmaxf(mx, v);
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      sm += __shfl_xor(sm, o);
+      mx = fmaxf(mx, __shfl_xor(mx, o));
+    }
+    if (sub == 0) {
+      s1[r] = in ? sm * (1.0f / 64.0f) : 0.f;
+      s2[r] = in ? mx : 0.f;
+    }
+  }
+  __syncthreads();
+  {
+    const int r = tid;
+    float a = bias ? cmisc[82] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      a = fmaf(cmisc[68 + k], s1[r + k - 3], a);
+      a = fmaf(cmisc[75 + k], s2[r + k - 3], a);
+    }
+    sa[r] = sigm(a);
+  }
+  __syncthreads();
+  // -- h = [identity +] u*ca*sa [relu], in place (rows outside [0, L) stay zero: u and identity are)
+  for (int k0 = 0; k0 < ID_ITERS; k0 += ID_GROUP) {
+    f32x4 idr[ID_GROUP];
+    if (res != RES_NONE) {
+#pragma unroll
+      for (int g = 0; g < ID_GROUP; ++g) idr[g] = hs_load(hs, ((w * 4 + rgrp + WAVES * 4 * (k0 + g)) * 64 + 4 * sub) * 4);
+    }
+#pragma unroll
+  for (int g = 0; g < ID_GROUP; ++g) {
+    const int r = w * 4 + rgrp + WAVES * 4 * (k0 + g);
+    const f32x4 u = Op<MODE>::load4(lds, r + GUARD, 4 * sub);
+    const float sr = sa[r];
+    f32x4 h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = (u[i] * cav[i]) * sr;
+    if (res != RES_NONE) {
+      h += idr[g];
+      if (res == RES_ADD_RELU)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[i] = fmaxf(h[i], 0.f);
+    }
+    const int p = tl.base + r;
+    if (p < 0 || p >= tl.L) h = f32x4{0.f, 0.f, 0.f, 0.f};
+    Op<MODE>::store4(lds, r + GUARD, 4 * sub, h);
+  }
+  }
+  __syncthreads();
+}
+
+template <int MODE, bool ADS>
+__global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restrict__ blob, const float* __restrict__ x,
+                                                        float* __restrict__ y, int L, TeamArgs ta) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  using G = Geo<MODE, true>;
+  const int team = blockIdx.x / ta.TT, tile = blockIdx.x - team * ta.TT;
+  const __amdgpu_buffer_rsrc_t hs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(ta.hsave + (size_t)blockIdx.x * WB * 64 * 4), 0, WB * 64 * 4, 0x00020000);
+  unsigned* ctr = ta.counters + (size_t)team * TEAM_CTR_STRIDE;
+  char* tslots = ta.slots + (size_t)team * 2 * ta.TT * SLOT_BYTES;
+  constexpr int NL = ADS ? 32 : 30;             // big layers
+  unsigned nbar = 0;
+  f32x4 id[16];
+  zero_guards(lds);
+  for (int64_t n = team; n < ta.n; n += ta.teams) {
+    Tile tl;
+    tl.lds = lds;
+    tl.x = x + (size_t)n * L;
+    tl.L = L;
+    tl.base = tile * ta.T - ta.halo;
+    tl.small = (const float*)blob;
+    tl.big = blob + SMALL_BYTES;
+    tl.layer = 0;
+    LayerA<MODE> a;
+    load_layer_a<MODE>(tl, 0, a);
+    // stats of u -> team -> apply.  The identity rows are fetched while the team assembles; the
+    // next layer's operands are loaded only now (held across this VALU-heavy code they spill).
+    auto cbam = [&](int slot, int res) {
+      char* mine = tslots + ((size_t)(nbar & 1) * ta.TT + tile) * SLOT_BYTES;
+      publish_stats<MODE>(tl, ta, mine, ctr);
+      team_wait(ta, ctr, (nbar + 1) * (unsigned)ta.TT);
+      apply_cbam<MODE>(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT_BYTES, slot, ADS, res, hs);
+      ++nbar;
+    };
+    stem<MODE>(tl, 0);
+    __syncthreads();
+    if (ADS) {
+      // ADSDN/train.py:160-167: cbam(relu(conv_ds x)); relu(conv1); relu(conv2); cbam;
+      // 15 x relu(cbam(bn2(conv2(relu(bn1(conv1 x))))) + x); conv_out
+      cbam(2, RES_NONE);
+      conv<MODE, RELU, G::S>(tl, 1, id, a, true);
+      conv<MODE, RELU, G::S>(tl, 1, id, a, true);
+      cbam(5, RES_NONE);
+      for (int b = 0; b < 15; ++b) {
+        save_identity<MODE>(tl, hs);
+        conv<MODE, RELU, G::S>(tl, 1, id, a, true);
+        conv<MODE, 0, G::S>(tl, 1, id, a, tl.layer + 1 < NL);
+        cbam(8 + 3 * b, RES_ADD_RELU);
+      }
+    } else {
+      // APIDN/train.py:150-159: h = relu(conv_ds x); 15 x x += cbam(bn(conv(relu(bn(conv x)))));
+      // sigmoid(conv_out(x + h))
+      for (int b = 0; b < 15; ++b) {
+        save_identity<MODE>(tl, hs);
+        conv<MODE, RELU, G::S>(tl, 1, id, a, true);
+        conv<MODE, 0, G::S>(tl, 1, id, a, tl.layer + 1 < NL);
+        cbam(2 + 3 * b, RES_ADD);
+      }
+      stem<MODE, true>(tl, 0);       // + h, recomputed from x
+      __syncthreads();
+    }
+    float v[HEAD_ROWS];
+    head<MODE>(tl, 1, v);
+    if (!ADS) {
+#pragma unroll
+      for (int k = 0; k < HEAD_ROWS; ++k) v[k] = sigm(v[k]);
+    }
+    store_out(tl, y, (int)n, v, ta.halo, ta.T);
+    __syncthreads();                 // the next spectrum's stem overwrites the rows the head read
+  }
+}
+
 }  // namespace cb
 
 // ---- host ----------------------------------------------------------------------------------------
@@ -271,9 +577,82 @@ static constexpr int64_t CBAM_CHUNK = 1024;       // spectra per pass (bounds th
 
 static size_t act_bytes(int64_t n, int64_t L) { return (size_t)n * L * 64 * sizeof(float); }
 
-size_t cbam_workspace_bytes(int, int, int64_t n, int64_t L) {
+// Team-persistent geometry: halo of the whole network (stem 1, conv 1 each, CBAM spatial conv 3,
+// head 1), TT tiles per spectrum, as many teams as fit one workgroup per CU.
+struct TeamGeo {
+  int halo, T, TT, teams;
+  size_t slots, counters, hsave, total;
+};
+static int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 0;
+  }
+  return cus;
+}
+static TeamGeo team_geo(int arch, int64_t L) {
+  TeamGeo g{};
+  g.halo = arch == ADSDN ? 1 + 3 + 2 + 3 + 15 * 5 + 1 : 1 + 15 * 5 + 1;
+  g.T = WB - 2 * g.halo;
+  g.TT = (int)((L + g.T - 1) / g.T);
+  const int cus = device_cus();
+  g.teams = cus > 0 ? cus / g.TT : 0;
+  const char* env = getenv("RDN_CBAM_SEGMENTS");       // diagnostics: force the per-segment path
+  if (env && env[0] == '1') g.teams = 0;
+  if (g.teams > 0) {
+    g.slots = (size_t)g.teams * 2 * g.TT * cb::SLOT_BYTES;
+    g.counters = (size_t)g.teams * cb::TEAM_CTR_STRIDE * 4;
+    g.hsave = (size_t)g.teams * g.TT * WB * 64 * 4;
+    g.total = g.slots + g.counters + g.hsave + 256 + 4 * 256;
+  }
+  return g;
+}
+
+size_t cbam_workspace_bytes(int arch, int, int64_t n, int64_t L) {
+  const TeamGeo g = team_geo(arch, L);
+  if (g.teams > 0) return g.total;
   const int64_t c = n < CBAM_CHUNK ? n : CBAM_CHUNK;
   return 4 * act_bytes(c, L) + 2 * (size_t)c * 64 * (sizeof(double) + sizeof(unsigned)) + 256;
+}
+
+// One launch for the whole network (see cb::team_forward).
+static hipError_t launch_team(int arch, int mode, const TeamGeo& g, const uint8_t* blob, const float* x, float* y,
+                              int64_t n, int L, void* ws, hipStream_t stream) {
+  using namespace cb;
+  typedef void (*team_kernel_t)(const uint8_t*, const float*, float*, int, TeamArgs);
+  const bool ads = arch == ADSDN;
+  team_kernel_t k;
+  if (mode == ip::MODE_F32) k = ads ? team_forward<ip::MODE_F32, true> : team_forward<ip::MODE_F32, false>;
+  else if (mode == ip::MODE_X3) k = ads ? team_forward<ip::MODE_X3, true> : team_forward<ip::MODE_X3, false>;
+  else k = ads ? team_forward<ip::MODE_B1, true> : team_forward<ip::MODE_B1, false>;
+  static bool attr_set[3][2] = {};
+  const int mi = mode == ip::MODE_F32 ? 0 : mode == ip::MODE_X3 ? 1 : 2;
+  if (!attr_set[mi][ads]) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SEG_LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_set[mi][ads] = true;
+  }
+  char* base = (char*)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
+  TeamArgs ta{};
+  ta.TT = g.TT;
+  ta.teams = g.teams;
+  ta.T = g.T;
+  ta.halo = g.halo;
+  ta.n = n;
+  ta.slots = base;
+  ta.counters = (unsigned*)(base + g.slots);
+  ta.hsave = base + ((g.slots + g.counters + 255) & ~(size_t)255);
+  ta.err = (unsigned*)(ta.hsave + g.hsave);
+  // counters and the error word start at 0 (the hand-off counts arrivals monotonically)
+  hipError_t e = hipMemsetAsync(ta.counters, 0, g.counters, stream);
+  if (e == hipSuccess) e = hipMemsetAsync(ta.err, 0, 4, stream);
+  if (e != hipSuccess) return e;
+  const int64_t teams = n < g.teams ? n : g.teams;    // never more teams than spectra
+  ta.teams = (int)teams;
+  hipLaunchKernelGGL(k, dim3((unsigned)(teams * g.TT)), dim3(THREADS), SEG_LDS_BYTES, stream, blob, x, y, L, ta);
+  return hipGetLastError();
 }
 
 typedef void (*seg_kernel_t)(const uint8_t*, const float*, float*, int, int, int, cb::Seg);
@@ -290,6 +669,11 @@ hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const f
     const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SEG_LDS_BYTES);
     if (e != hipSuccess) return e;
     attr_set[mi] = true;
+  }
+  const TeamGeo tg = team_geo(arch, L);
+  if (tg.teams > 0) {
+    if (ws_bytes < tg.total) return hipErrorInvalidValue;
+    return launch_team(arch, mode, tg, blob, x, y, n, L, ws, stream);
   }
   const bool adsdn = arch == ADSDN;
   const int64_t chunk = n < CBAM_CHUNK ? n : CBAM_CHUNK;
