@@ -169,7 +169,7 @@ __device__ void prologue_stem(Tile& tl, const Seg& sg, int n) {
   stem<MODE>(tl, 0);
   __syncthreads();
   if (!sg.store_h) return;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, sub = lane & 15, rgrp = lane >> 4;
+  const int tid = opaque_tid(), lane = tid & 63, w = tid >> 6, sub = lane & 15, rgrp = lane >> 4;
   const int H = sg.halo, T = WB - 2 * H;
   for (int r = w * 4 + rgrp; r < WB; r += WAVES * 4) {
     const int p = tl.base + r;
@@ -182,7 +182,7 @@ __device__ void prologue_stem(Tile& tl, const Seg& sg, int n) {
 template <int MODE>
 __device__ void epilogue_store(Tile& tl, const Seg& sg, int n) {
   char* lds = tl.lds;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, sub = lane & 15, rgrp = lane >> 4;
+  const int tid = opaque_tid(), lane = tid & 63, w = tid >> 6, sub = lane & 15, rgrp = lane >> 4;
   const int H = sg.halo, T = WB - 2 * H;
   double sm[4] = {0, 0, 0, 0};
   float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
@@ -214,8 +214,8 @@ __device__ void epilogue_store(Tile& tl, const Seg& sg, int n) {
     }
   }
   __syncthreads();
-  if (threadIdx.x < 64) {
-    const int c = threadIdx.x;
+  if (tid < 64) {
+    const int c = tid;
     double s = 0.0;
     unsigned m = 0;
     for (int k = 0; k < WAVES; ++k) {
@@ -295,6 +295,31 @@ struct TeamArgs {
   unsigned* counters;   // [teams][TEAM_CTR_STRIDE], zeroed before the launch
   char* hsave;          // [teams * TT][WB][64] f32
   unsigned* err;
+  unsigned long long* stamps;   // RDN_TEAM_STAMPS diagnostics: [grid][NSTAMP] cycle sums per phase
+};
+#ifndef RDN_TEAM_STAMPS
+#define RDN_TEAM_STAMPS 0
+#endif
+constexpr int NSTAMP = 16;
+constexpr int STAMP_BYTES = RDN_TEAM_STAMPS ? 256 * NSTAMP * 8 : 0;
+
+// diagnostics (RDN_TEAM_STAMPS=1, tools/team_stamps.py): s_memtime deltas summed per phase by
+// wave 0; compiled out otherwise
+struct Stamps {
+  unsigned long long acc[NSTAMP], t;
+  __device__ __forceinline__ void init() {
+    if (RDN_TEAM_STAMPS) {
+      for (int k = 0; k < NSTAMP; ++k) acc[k] = 0;
+      t = __builtin_amdgcn_s_memtime();
+    }
+  }
+  __device__ __forceinline__ void operator()(int k) {
+    if (RDN_TEAM_STAMPS) {
+      const unsigned long long n = __builtin_amdgcn_s_memtime();
+      acc[k] += n - t;
+      t = n;
+    }
+  }
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -307,29 +332,81 @@ __device__ __forceinline__ f32x4 hs_load(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
 }
 
-// block input x (all WB tile rows) -> identity buffer
+// Row k (0 .. 15) of the pointwise passes for lane group rgrp of wave w: 16 lanes x 4 channels per
+// row, 32 rows per pass step.  fp32 rows (16 x 16 B) take 4 consecutive rows per wave (conflict-free
+// ds_read_b128); the bf16 planes (16 x 8 B, ds_read_b64 in 32-lane groups) pair rows r and r + 4,
+// whose swizzles put the plane in opposite halves of the 256 B of banks.
 template <int MODE>
-__device__ void save_identity(const Tile& tl, __amdgpu_buffer_rsrc_t hs) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, sub = lane & 15, rgrp = lane >> 4;
-  for (int r = w * 4 + rgrp; r < WB; r += WAVES * 4) hs_store(hs, (r * 64 + 4 * sub) * 4, Op<MODE>::load4(tl.lds, r + GUARD, 4 * sub));
+__device__ __forceinline__ int pw_row(int w, int rgrp, int k) {
+  if (MODE == MODE_F32) return 32 * k + 4 * w + rgrp;
+  return 32 * k + 8 * (w >> 1) + 2 * (w & 1) + 4 * (rgrp & 1) + (rgrp >> 1);
+}
+
+// The ResidualBlock identity (the block input, all WB tile rows).  Plain bf16 keeps it in the free
+// lo plane of its own LDS row (the activation is bf16 there, so the copy is exact); fp32 and
+// split-bf16 park it as fp32 in the workgroup's buffer in memory.
+template <int MODE>
+__device__ __forceinline__ void id_store(char* lds, __amdgpu_buffer_rsrc_t hs, int r, int sub, f32x4 h) {
+  if (MODE == MODE_B1) *(bf16x4*)(lds + off_f32(r + GUARD, 128 + 8 * sub)) = __builtin_convertvector(h, bf16x4);
+  else hs_store(hs, (r * 64 + 4 * sub) * 4, h);
+}
+template <int MODE>
+__device__ __forceinline__ f32x4 id_load(const char* lds, __amdgpu_buffer_rsrc_t hs, int r, int sub) {
+  if (MODE == MODE_B1) return __builtin_convertvector(*(const bf16x4*)(lds + off_f32(r + GUARD, 128 + 8 * sub)), f32x4);
+  return hs_load(hs, (r * 64 + 4 * sub) * 4);
+}
+
+// block input (all WB tile rows) -> identity (used after the stem; later blocks save it from the
+// CBAM write-back that produces it)
+template <int MODE>
+__device__ __forceinline__ void save_identity(const Tile& tl, __amdgpu_buffer_rsrc_t hs) {
+  const int tid = opaque_tid(), lane = tid & 63, w = tid >> 6, sub = lane & 15, rgrp = lane >> 4;
+#pragma unroll 4
+  for (int k = 0; k < WB / 32; ++k) {
+    const int r = pw_row<MODE>(w, rgrp, k);
+    id_store<MODE>(tl.lds, hs, r, sub, Op<MODE>::load4(tl.lds, r + GUARD, 4 * sub));
+  }
+}
+
+// 8 channels [8k, 8k+8) of tile row r as f32
+template <int MODE>
+__device__ __forceinline__ void load8(const char* lds, int r, int k, float (&v)[8]) {
+  const int pr = r + GUARD;
+  if (MODE == MODE_F32) {
+    const f32x4 a = *(const f32x4*)(lds + off_f32(pr, 32 * k)), b = *(const f32x4*)(lds + off_f32(pr, 32 * k + 16));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = a[i];
+      v[4 + i] = b[i];
+    }
+  } else {
+    const bf16x8 hi = *(const bf16x8*)(lds + off_f32(pr, 16 * k));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)hi[i];
+    if (MODE == MODE_X3) {
+      const bf16x8 lo = *(const bf16x8*)(lds + off_f32(pr, 128 + 16 * k));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] += (float)lo[i];
+    }
+  }
 }
 
 // per-channel sum / max of u over the tile's own positions -> slot (sc1); arrive at the counter
 template <int MODE>
-__device__ void publish_stats(const Tile& tl, const TeamArgs& ta, char* slot, unsigned* ctr) {
+__device__ __forceinline__ void publish_stats(const Tile& tl, const TeamArgs& ta, char* slot, unsigned* ctr, Stamps& st) {
   char* lds = tl.lds;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, sub = lane & 15, rgrp = lane >> 4;
+  const int tid = opaque_tid(), lane = tid & 63, w = tid >> 6, sub = lane & 15, rgrp = lane >> 4;
   const int H = ta.halo, T = ta.T;
-  double sm[4] = {0, 0, 0, 0};
-  float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  for (int r = H + w * 4 + rgrp; r < H + T; r += WAVES * 4) {
-    if (tl.base + r >= tl.L) break;
+  const int rend = H + min(T, tl.L - tl.base - H);     // the last tile of a spectrum ends at L
+  // fp32 partials over <= T / 32 rows per lane, fp64 from the cross-wave sum on
+  f32x4 sm = {0.f, 0.f, 0.f, 0.f}, mx = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll 4
+  for (int k = 0; k < WB / 32; ++k) {
+    const int r = H + pw_row<MODE>(w, rgrp, k);
+    if (r >= rend) break;              // pw_row is increasing in k
     const f32x4 u = Op<MODE>::load4(lds, r + GUARD, 4 * sub);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      sm[i] += (double)u[i];
-      mx[i] = fmaxf(mx[i], u[i]);
-    }
+    sm += u;
+    mx = __builtin_elementwise_max(mx, u);
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -338,7 +415,7 @@ __device__ void publish_stats(const Tile& tl, const TeamArgs& ta, char* slot, un
       mx[i] = fmaxf(mx[i], __shfl_xor(mx[i], o));
     }
   }
-  double* rs = (double*)(lds + RED_OFF);
+  float* rs = (float*)(lds + RED_OFF);
   unsigned* rm = (unsigned*)(lds + RED_OFF + 8 * 64 * 8);
   if (rgrp == 0) {
 #pragma unroll
@@ -347,13 +424,16 @@ __device__ void publish_stats(const Tile& tl, const TeamArgs& ta, char* slot, un
       rm[w * 64 + 4 * sub + i] = f2ord(mx[i]);
     }
   }
+  st(8);
   __syncthreads();
-  if (threadIdx.x < 64) {
-    const int c = threadIdx.x;
+  st(9);
+  if (tid < 64) {
+    const int c = tid;
     double s = 0.0;
     unsigned m = 0;
+#pragma unroll
     for (int k = 0; k < WAVES; ++k) {
-      s += rs[k * 64 + c];
+      s += (double)rs[k * 64 + c];
       m = max(m, rm[k * 64 + c]);
     }
     __hip_atomic_store((double*)slot + c, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -364,7 +444,7 @@ __device__ void publish_stats(const Tile& tl, const TeamArgs& ta, char* slot, un
 }
 
 // the team has arrived at `target`: lane 0 polls (sc1), the workgroup barrier releases the rest
-__device__ void team_wait(const TeamArgs& ta, unsigned* ctr, unsigned target) {
+__device__ __forceinline__ void team_wait(const TeamArgs& ta, unsigned* ctr, unsigned target) {
   if (threadIdx.x == 0) {
     unsigned it = 0;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -380,13 +460,24 @@ __device__ void team_wait(const TeamArgs& ta, unsigned* ctr, unsigned target) {
 
 // Apply a CBAM whose statistics sit in the team's slots (`slots0`: TT slots of this barrier) to u
 // in the tile: h = [identity +] u*ca*sa [then ReLU] (ADSDN/train.py:113-116,143-147;
-// APIDN/train.py:113-116,154-156), written over u.
+// APIDN/train.py:113-116,154-156), written over u (and, with save_next, as the next block's
+// identity).
 constexpr int ID_ITERS = WB / (WAVES * 4);          // rows per thread in the pointwise pass (16)
-constexpr int ID_GROUP = 4;                          // identity loads in flight per thread
+#ifndef RDN_CBAM_RELOAD_A
+#define RDN_CBAM_RELOAD_A 0
+#endif
+// identity rows fetched ahead of the spatial pass (the rest at the write-back): all 16 for fp32,
+// 8 for split-bf16 (16 spill there; measured 18.8k vs 16.5k APIDN spectra/s); plain bf16 keeps
+// its identity in LDS
+#ifdef RDN_CBAM_ID_PRE
+template <int MODE> constexpr int ID_PRE = RDN_CBAM_ID_PRE;
+#else
+template <int MODE> constexpr int ID_PRE = MODE == MODE_F32 ? 16 : 8;
+#endif
 
 template <int MODE>
-__device__ void apply_cbam(const Tile& tl, const TeamArgs& ta, const char* slots0, int cbam_slot, bool bias, int res,
-                           __amdgpu_buffer_rsrc_t hs) {
+__device__ __forceinline__ void apply_cbam(const Tile& tl, const TeamArgs& ta, const char* slots0, int cbam_slot, bool bias, int res,
+                           bool save_next, __amdgpu_buffer_rsrc_t hs, Stamps& st) {
   char* lds = tl.lds;
   float* s1 = (float*)(lds + S1_OFF) + 3;       // index -3 .. 514
   float* s2 = (float*)(lds + S2_OFF) + 3;
@@ -394,69 +485,117 @@ __device__ void apply_cbam(const Tile& tl, const TeamArgs& ta, const char* slots
   float* ca = (float*)(lds + CA_OFF);
   float* h1 = (float*)(lds + H1_OFF);
   double* red = (double*)(lds + RED_OFF);        // pooled avg / max per channel (2 x 64)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = opaque_tid(), lane = tid & 63, w = tid >> 6;
   const float* cw = tl.small + cbam_slot * SMALL_SLOT_FLOATS;      // fc.0.weight [4][64]
   const float* cw2 = cw + SMALL_SLOT_FLOATS;                       // fc.2.weight [64][4]
   const float* cmisc = cw2 + SMALL_SLOT_FLOATS;                    // fc.0.bias[4], fc.2.bias[64], sa.w[2][7], sa.b
+  // the CBAM's weights, fetched under the statistics round trip
+  const float cwv = cw[(w & 3) * 64 + lane];                       // hidden unit w & 3, channel lane
+  const float b1 = bias ? cmisc[w & 3] : 0.f;
+  const f32x4 cw2v = *(const f32x4*)(cw2 + 4 * lane);              // channel lane's 4 hidden weights
+  const float b2 = bias ? cmisc[4 + lane] : 0.f;
 
-  // -- the spectrum's per-channel mean and max: reduce the TT slots in tile order
-  if (tid < 64) {
-    double s = 0.0;
-    unsigned m = 0;
-    for (int t = 0; t < ta.TT; ++t) {
-      const char* sl = slots0 + (size_t)t * SLOT_BYTES;
-      s += __hip_atomic_load((const double*)sl + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      m = max(m, __hip_atomic_load((const unsigned*)(sl + 512) + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  // -- the spectrum's per-channel mean and max over the TT slots: 8 tile-strided partials per
+  //    channel (all waves, sc1 buffer loads issued together: they are L2 / fabric round trips),
+  //    then combined in a fixed order (deterministic)
+  {
+    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slots0, 0, ta.TT * SLOT_BYTES, 0x00020000);
+    const int c = tid & 63, part = tid >> 6;             // part = 0..7 (WAVES)
+    double sp = 0.0;
+    unsigned mp = 0;
+    constexpr int PER = 8;                               // slots per batch per thread
+    for (int t0 = part; t0 < ta.TT; t0 += WAVES * PER) {
+      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+      u32x2 sv[PER];
+      unsigned mv[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int t = t0 + WAVES * k;
+        const int off = (t < ta.TT ? t : 0) * SLOT_BYTES;
+        sv[k] = __builtin_amdgcn_raw_buffer_load_b64(sr, off + 8 * c, 0, 16);
+        mv[k] = __builtin_amdgcn_raw_buffer_load_b32(sr, off + 512 + 4 * c, 0, 16);
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        if (t0 + WAVES * k < ta.TT) {
+          sp += __builtin_bit_cast(double, sv[k]);
+          mp = max(mp, mv[k]);
+        }
+      }
     }
-    red[tid] = (double)(float)(s / (double)tl.L);
-    red[64 + tid] = (double)ord2f(m);
+    double* rs = (double*)(lds + S1_OFF);               // 8 x 64 partials in the spatial-pass scratch
+    unsigned* rm = (unsigned*)(lds + SA_OFF);           // (S1+S2: 4160 B, SA: 2048 B; refilled below)
+    static_assert(S2_OFF + 520 * 4 - S1_OFF >= 8 * 64 * 8 && CA_OFF - SA_OFF >= 8 * 64 * 4, "partials fit");
+    rs[part * 64 + c] = sp;
+    rm[part * 64 + c] = mp;
+    __syncthreads();
+    if (tid < 64) {
+      double sum = 0.0;
+      unsigned m = 0;
+#pragma unroll
+      for (int k = 0; k < WAVES; ++k) {
+        sum += rs[k * 64 + tid];
+        m = max(m, rm[k * 64 + tid]);
+      }
+      red[tid] = (double)(float)(sum / (double)tl.L);
+      red[64 + tid] = (double)ord2f(m);
+    }
   }
   __syncthreads();
-  // -- channel attention: hidden units of the shared MLP for the avg- and max-pooled vectors
-  if (tid < 8) {
-    const int j = tid & 3, which = tid >> 2;        // which: 0 = avg, 1 = max
-    float a = bias ? cmisc[j] : 0.f;
-    for (int c = 0; c < 64; ++c) a = fmaf(cw[j * 64 + c], (float)red[which * 64 + c], a);
-    h1[tid] = fmaxf(a, 0.f);
+  st(10);
+  // -- channel attention: hidden unit (w & 3) of the shared MLP for the avg (w < 4) or max pooled
+  //    vector, one wave each (64 lanes = 64 channels, butterfly sum)
+  {
+    float a = cwv * (float)red[(w >> 2) * 64 + lane];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    if (lane == 0) h1[w] = fmaxf(a + b1, 0.f);
   }
   __syncthreads();
   if (tid < 64) {
-    float oa = bias ? cmisc[4 + tid] : 0.f, om = oa;
+    float oa = b2, om = b2;
+#pragma unroll
     for (int j = 0; j < 4; ++j) {
-      oa = fmaf(cw2[tid * 4 + j], h1[j], oa);
-      om = fmaf(cw2[tid * 4 + j], h1[4 + j], om);
+      oa = fmaf(cw2v[j], h1[j], oa);
+      om = fmaf(cw2v[j], h1[4 + j], om);
     }
     ca[tid] = sigm(oa + om);
   }
   __syncthreads();
+  st(11);
 
-  // -- spatial statistics of u*ca per tile row (rows beyond the tile: 0; they feed only halo rows)
+  // -- identities of this thread's pointwise rows, in flight during the spatial pass
   const int sub = lane & 15, rgrp = lane >> 4;
-  const f32x4 cav = *(const f32x4*)(ca + 4 * sub);
-  for (int r = w * 4 + rgrp - 3; r < WB + 3; r += WAVES * 4) {
+  f32x4 idr[ID_ITERS];
+  if (MODE != MODE_B1 && res != RES_NONE) {
+#pragma unroll
+    for (int k = 0; k < ID_PRE<MODE>; ++k) idr[k] = hs_load(hs, (pw_row<MODE>(w, rgrp, k) * 64 + 4 * sub) * 4);
+  }
+  // -- spatial statistics of u*ca: one tile row per thread (rows beyond the tile: 0; they feed
+  //    only halo rows)
+  for (int r = tid - 3; r < WB + 3; r += THREADS) {
     const int p = tl.base + r;
     const bool in = p >= 0 && p < tl.L && r >= 0 && r < WB;   // conv7 zero-pads the [mean; max] map
     float sm = 0.f, mx = -INFINITY;
     if (in) {
-      const f32x4 u = Op<MODE>::load4(lds, r + GUARD, 4 * sub);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float v = u[i] * cav[i];
-        sm += v;
-        mx = fmaxf(mx, v);
+      for (int k = 0; k < 8; ++k) {
+        float u[8];
+        load8<MODE>(lds, r, k, u);
+        const f32x4 c0 = *(const f32x4*)(ca + 8 * k), c1 = *(const f32x4*)(ca + 8 * k + 4);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float v = u[i] * (i < 4 ? c0[i] : c1[i - 4]);
+          sm += v;
+          mx = fmaxf(mx, v);
+        }
       }
     }
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      sm += __shfl_xor(sm, o);
-      mx = fmaxf(mx, __shfl_xor(mx, o));
-    }
-    if (sub == 0) {
-      s1[r] = in ? sm * (1.0f / 64.0f) : 0.f;
-      s2[r] = in ? mx : 0.f;
-    }
+    s1[r] = in ? sm * (1.0f / 64.0f) : 0.f;
+    s2[r] = in ? mx : 0.f;
   }
   __syncthreads();
+  st(12);
   {
     const int r = tid;
     float a = bias ? cmisc[82] : 0.f;
@@ -468,31 +607,25 @@ __device__ void apply_cbam(const Tile& tl, const TeamArgs& ta, const char* slots
     sa[r] = sigm(a);
   }
   __syncthreads();
+  st(13);
   // -- h = [identity +] u*ca*sa [relu], in place (rows outside [0, L) stay zero: u and identity are)
-  for (int k0 = 0; k0 < ID_ITERS; k0 += ID_GROUP) {
-    f32x4 idr[ID_GROUP];
-    if (res != RES_NONE) {
+  const f32x4 cav = *(const f32x4*)(ca + 4 * sub);
 #pragma unroll
-      for (int g = 0; g < ID_GROUP; ++g) idr[g] = hs_load(hs, ((w * 4 + rgrp + WAVES * 4 * (k0 + g)) * 64 + 4 * sub) * 4);
-    }
-#pragma unroll
-  for (int g = 0; g < ID_GROUP; ++g) {
-    const int r = w * 4 + rgrp + WAVES * 4 * (k0 + g);
+  for (int k = 0; k < ID_ITERS; ++k) {
+    const int r = pw_row<MODE>(w, rgrp, k);
     const f32x4 u = Op<MODE>::load4(lds, r + GUARD, 4 * sub);
     const float sr = sa[r];
     f32x4 h;
 #pragma unroll
     for (int i = 0; i < 4; ++i) h[i] = (u[i] * cav[i]) * sr;
     if (res != RES_NONE) {
-      h += idr[g];
-      if (res == RES_ADD_RELU)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) h[i] = fmaxf(h[i], 0.f);
+      h += MODE == MODE_B1 || k >= ID_PRE<MODE> ? id_load<MODE>(lds, hs, r, sub) : idr[k];
+      if (res == RES_ADD_RELU) h = __builtin_elementwise_max(h, f32x4{0.f, 0.f, 0.f, 0.f});
     }
     const int p = tl.base + r;
     if (p < 0 || p >= tl.L) h = f32x4{0.f, 0.f, 0.f, 0.f};
     Op<MODE>::store4(lds, r + GUARD, 4 * sub, h);
-  }
+    if (save_next) id_store<MODE>(lds, hs, r, sub, h);
   }
   __syncthreads();
 }
@@ -508,8 +641,13 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
   unsigned* ctr = ta.counters + (size_t)team * TEAM_CTR_STRIDE;
   char* tslots = ta.slots + (size_t)team * 2 * ta.TT * SLOT_BYTES;
   constexpr int NL = ADS ? 32 : 30;             // big layers
+  // the next layer's weights: prefetched by the conv before a CBAM (held across it), or loaded
+  // after it (RDN_CBAM_RELOAD_A: frees their VGPRs during the CBAM)
+  constexpr bool RELOAD_A = RDN_CBAM_RELOAD_A;
   unsigned nbar = 0;
   f32x4 id[16];
+  Stamps stamp;
+  stamp.init();
   zero_guards(lds);
   for (int64_t n = team; n < ta.n; n += ta.teams) {
     Tile tl;
@@ -524,36 +662,42 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
     load_layer_a<MODE>(tl, 0, a);
     // stats of u -> team -> apply.  The identity rows are fetched while the team assembles; the
     // next layer's operands are loaded only now (held across this VALU-heavy code they spill).
-    auto cbam = [&](int slot, int res) {
+    auto cbam = [&](int slot, int res, bool save_next) {
       char* mine = tslots + ((size_t)(nbar & 1) * ta.TT + tile) * SLOT_BYTES;
-      publish_stats<MODE>(tl, ta, mine, ctr);
+      publish_stats<MODE>(tl, ta, mine, ctr, stamp);
+      stamp(3);
       team_wait(ta, ctr, (nbar + 1) * (unsigned)ta.TT);
-      apply_cbam<MODE>(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT_BYTES, slot, ADS, res, hs);
+      stamp(4);
+      apply_cbam<MODE>(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT_BYTES, slot, ADS, res, save_next, hs, stamp);
+      stamp(5);
       ++nbar;
+      if (RELOAD_A && tl.layer < NL) load_layer_a<MODE>(tl, tl.layer, a);
     };
     stem<MODE>(tl, 0);
     __syncthreads();
     if (ADS) {
       // ADSDN/train.py:160-167: cbam(relu(conv_ds x)); relu(conv1); relu(conv2); cbam;
       // 15 x relu(cbam(bn2(conv2(relu(bn1(conv1 x))))) + x); conv_out
-      cbam(2, RES_NONE);
+      cbam(2, RES_NONE, false);
       conv<MODE, RELU, G::S>(tl, 1, id, a, true);
-      conv<MODE, RELU, G::S>(tl, 1, id, a, true);
-      cbam(5, RES_NONE);
+      conv<MODE, RELU, G::S>(tl, 1, id, a, !RELOAD_A);
+      cbam(5, RES_NONE, true);                   // block 0's identity
       for (int b = 0; b < 15; ++b) {
-        save_identity<MODE>(tl, hs);
         conv<MODE, RELU, G::S>(tl, 1, id, a, true);
-        conv<MODE, 0, G::S>(tl, 1, id, a, tl.layer + 1 < NL);
-        cbam(8 + 3 * b, RES_ADD_RELU);
+        conv<MODE, 0, G::S>(tl, 1, id, a, !RELOAD_A && tl.layer + 1 < NL);
+        cbam(8 + 3 * b, RES_ADD_RELU, b < 14);
       }
     } else {
       // APIDN/train.py:150-159: h = relu(conv_ds x); 15 x x += cbam(bn(conv(relu(bn(conv x)))));
       // sigmoid(conv_out(x + h))
+      save_identity<MODE>(tl, hs);
       for (int b = 0; b < 15; ++b) {
-        save_identity<MODE>(tl, hs);
+        stamp(7);
         conv<MODE, RELU, G::S>(tl, 1, id, a, true);
-        conv<MODE, 0, G::S>(tl, 1, id, a, tl.layer + 1 < NL);
-        cbam(2 + 3 * b, RES_ADD);
+        stamp(1);
+        conv<MODE, 0, G::S>(tl, 1, id, a, !RELOAD_A && tl.layer + 1 < NL);
+        stamp(2);
+        cbam(2 + 3 * b, RES_ADD, b < 14);
       }
       stem<MODE, true>(tl, 0);       // + h, recomputed from x
       __syncthreads();
@@ -566,7 +710,10 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
     }
     store_out(tl, y, (int)n, v, ta.halo, ta.T);
     __syncthreads();                 // the next spectrum's stem overwrites the rows the head read
+    stamp(6);
   }
+  if (RDN_TEAM_STAMPS && threadIdx.x == 0 && ta.stamps)
+    for (int k = 0; k < NSTAMP; ++k) ta.stamps[(size_t)blockIdx.x * NSTAMP + k] = stamp.acc[k];
 }
 
 }  // namespace cb
@@ -605,7 +752,7 @@ static TeamGeo team_geo(int arch, int64_t L) {
     g.slots = (size_t)g.teams * 2 * g.TT * cb::SLOT_BYTES;
     g.counters = (size_t)g.teams * cb::TEAM_CTR_STRIDE * 4;
     g.hsave = (size_t)g.teams * g.TT * WB * 64 * 4;
-    g.total = g.slots + g.counters + g.hsave + 256 + 4 * 256;
+    g.total = g.slots + g.counters + g.hsave + 256 + 4 * 256 + cb::STAMP_BYTES;
   }
   return g;
 }
@@ -645,6 +792,7 @@ static hipError_t launch_team(int arch, int mode, const TeamGeo& g, const uint8_
   ta.counters = (unsigned*)(base + g.slots);
   ta.hsave = base + ((g.slots + g.counters + 255) & ~(size_t)255);
   ta.err = (unsigned*)(ta.hsave + g.hsave);
+  ta.stamps = cb::STAMP_BYTES ? (unsigned long long*)((char*)ws + g.total - cb::STAMP_BYTES) : nullptr;
   // counters and the error word start at 0 (the hand-off counts arrivals monotonically)
   hipError_t e = hipMemsetAsync(ta.counters, 0, g.counters, stream);
   if (e == hipSuccess) e = hipMemsetAsync(ta.err, 0, 4, stream);

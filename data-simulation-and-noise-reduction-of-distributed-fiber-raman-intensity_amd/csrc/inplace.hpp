@@ -61,6 +61,15 @@ struct Tile {
 
 __device__ __forceinline__ bool in_range(int p, int L) { return p >= 0 && p < L; }
 
+// Thread index the compiler cannot treat as loop-invariant: per-lane addresses derived from it are
+// recomputed where they are used instead of being hoisted out of the callers' layer / spectrum
+// loops (where, with 256 VGPRs taken by the conv, they are spilled to scratch and reloaded).
+__device__ __forceinline__ int opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 // ---- operand traits -------------------------------------------------------------------------
 template <int MODE> struct Op;
 
@@ -203,7 +212,7 @@ template <int MODE, bool ACCUM = false, int NBK = 4>
 __device__ __forceinline__ void stem(const Tile& tl, int slot) {
   using TG = TileGeo<NBK>;
   const cfloat* sw = small_slot(tl, slot);
-  for (int j = threadIdx.x; j < TG::WB; j += THREADS) {
+  for (int j = opaque_tid(); j < TG::WB; j += THREADS) {
   const int pr = TG::row(j);
   const int p = tl.base + j;
   const float xm = in_range(p - 1, tl.L) ? tl.x[p - 1] : 0.f;
@@ -239,7 +248,7 @@ __device__ __forceinline__ void head(const Tile& tl, int slot, float (&out)[HEAD
   const cfloat* hw = small_slot(tl, slot);
 #pragma unroll
   for (int k = 0; k < HEAD_ROWS; ++k) {
-  const int j = threadIdx.x + THREADS * k;
+  const int j = opaque_tid() + THREADS * k;
   out[k] = 0.f;
   if (j >= TG::WB) continue;
   float a = hw[192];
@@ -284,7 +293,7 @@ __device__ __forceinline__ f32x4 load_bias(const uint8_t* wl, int m) {
 
 template <int MODE>
 __device__ __forceinline__ void load_layer_a(const Tile& tl, int layer, LayerA<MODE>& a) {
-  const int mp = (threadIdx.x >> 6) & 1, lane = threadIdx.x & 63;
+  const int tid = opaque_tid(), mp = (tid >> 6) & 1, lane = tid & 63;
   const uint8_t* wl = tl.big + (size_t)layer * BIG_BYTES;
 #pragma unroll
   for (int mm = 0; mm < IP_MT; ++mm) {
@@ -309,7 +318,8 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   using TG = TileGeo<NBK>;
   constexpr int NB = NBK, NT = IP_NT, MT = IP_MT, BR = IP_BR;
   constexpr int TS = O::KSTEPS / 3;                  // k-steps per tap
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tid = opaque_tid();
+  const int lane = tid & 63, w = tid >> 6;
   const int mp = w & 1, nq = w >> 1;
   const int q = lane >> 4, c16 = lane & 15;
   const uint8_t* wcur = tl.big + (size_t)tl.layer * BIG_BYTES;
@@ -491,7 +501,7 @@ __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const 
 __device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, const float (&v)[HEAD_ROWS], int halo, int T) {
 #pragma unroll
   for (int k = 0; k < HEAD_ROWS; ++k) {
-    const int j = threadIdx.x + THREADS * k;
+    const int j = opaque_tid() + THREADS * k;
     const int p = tl.base + j;
     if (j >= halo && j < halo + T && p < tl.L) y[(size_t)n * tl.L + p] = v[k];
   }

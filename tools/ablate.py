@@ -18,7 +18,9 @@ OUT = os.path.join(ROOT, "tools", "ablate_build")
 VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "nomfma": "-DRDN_ABLATE_NOMFMA", "nostore": "-DRDN_ABLATE_NOSTORE", "noaload": "-DRDN_ABLATE_NOALOAD",
             "pf3": "-DRDN_H16_PF=3", "ieee": "", "nospread": "-DRDN_IP_SPREAD_STORE=0", "prio": "-DRDN_IP_PRIO=1",
-            "prionospread": "-DRDN_IP_PRIO=1 -DRDN_IP_SPREAD_STORE=0"}
+            "prionospread": "-DRDN_IP_PRIO=1 -DRDN_IP_SPREAD_STORE=0", "stamps": "-DRDN_TEAM_STAMPS=1",
+            "stamps_pre0": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_ID_PRE=0", "stamps_reload": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_RELOAD_A=1",
+            "stamps_pre16": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_ID_PRE=16"}
 
 
 def build():

@@ -1,0 +1,78 @@
+"""Per-phase cycle breakdown of the team-persistent CBAM kernel (diagnostic, not part of the product).
+
+Uses the `stamps` variant of tools/ablate.py (cbam.hip built with -DRDN_TEAM_STAMPS=1): wave 0 of every
+workgroup sums s_memtime deltas per phase into the last 16 KiB of the forward workspace.
+
+    python tools/ablate.py build stamps      # build container
+    python tools/team_stamps.py [ARCH] [DTYPE] [L]   # GPU box
+"""
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fiber-raman-intensity_amd"))
+
+PHASES = ["save_identity", "conv1", "conv2", "publish:atomic", "wait", "apply:pointwise", "stem/head/store",
+          "loop-other", "publish:rows", "publish:barrier", "apply:slots", "apply:mlp", "apply:spatial-stats",
+          "apply:sa-conv"]
+NSTAMP = 16
+
+
+def main():
+    import raman_mi355x as R
+    from raman_mi355x import _lib, engine
+    arch = sys.argv[1] if len(sys.argv) > 1 else "APIDN"
+    dtype = sys.argv[2] if len(sys.argv) > 2 else "bf16x3"
+    L = int(sys.argv[3]) if len(sys.argv) > 3 else 10000
+    variant = sys.argv[4] if len(sys.argv) > 4 else "stamps"
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "ablate_build", f"lib_{variant}.so"))
+    for fn, (args, res) in _lib._SIGNATURES.items():
+        getattr(lib, fn).argtypes = args
+        getattr(lib, fn).restype = res
+    dev = torch.device("cuda")
+    B = 1024
+    _, noisy, _, _ = engine.generate(B, 3, signal_length=L, device=dev)
+    x = noisy.view(B, 1, L)
+    y = torch.empty_like(x)
+    torch.manual_seed(0)
+    model = R.MODELS[arch]()
+    names = engine.param_names(arch)
+    sd = model.state_dict()
+    host = [sd[k].detach().float().contiguous() for k in names]
+    ptrs = (ctypes.c_void_p * len(host))(*[t.data_ptr() for t in host])
+    numels = (ctypes.c_int64 * len(host))(*[t.numel() for t in host])
+    a, code = engine.ARCH_ID[arch], engine.DTYPE_ID[dtype]
+    size = ctypes.c_size_t()
+    assert lib.rdn_packed_size(a, code, ctypes.byref(size)) == 0
+    blob = torch.empty(size.value, dtype=torch.uint8)
+    assert lib.rdn_pack(a, code, ptrs, numels, len(host), ctypes.c_void_p(blob.data_ptr()), size.value) == 0
+    packed = blob.to(dev)
+    assert lib.rdn_workspace_size(a, code, B, L, ctypes.byref(size)) == 0
+    ws = torch.zeros(size.value, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for it in range(2):
+        e0.record()
+        rc = lib.rdn_forward(a, code, packed.data_ptr(), x.data_ptr(), y.data_ptr(), B, L,
+                             ctypes.c_void_p(ws.data_ptr()), size.value, stream)
+        e1.record()
+        assert rc == 0, lib.rdn_last_error()
+        torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    st = ws[-256 * NSTAMP * 8:].view(torch.int64).view(256, NSTAMP).cpu().double()
+    used = st.sum(1) > 0
+    st = st[used]
+    tot = st.sum(1)
+    print(f"[{variant}] {arch} {dtype} L={L} B={B}: {ms:.2f} ms, {B / ms * 1e3:,.0f} spectra/s, {int(used.sum())} workgroups")
+    print(f"total cycles per WG: mean {tot.mean():.3e} min {tot.min():.3e} max {tot.max():.3e} "
+          f"(=> {tot.mean() / (ms * 1e-3) / 1e9:.3f} G s_memtime ticks/s)")
+    for k, p in enumerate(PHASES):
+        c = st[:, k]
+        print(f"  {p:18s} mean {c.mean():.3e} ({100 * c.mean() / tot.mean():5.1f}%)  min {c.min():.3e} max {c.max():.3e}")
+
+
+if __name__ == "__main__":
+    main()
