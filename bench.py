@@ -28,7 +28,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "denoised spectra/sec (node) RRCDNet bf16/fp32 at 1/2/4/8 GPU; % MFMA peak"
 # Dense MFMA peaks, MI355X_MICROARCH.md §Chip-level parameters (spec values)
-PEAK_TFLOPS = {"bf16": 2500.0, "bf16x3": 2500.0, "fp32": 157.3}
+PEAK_TFLOPS = {"bf16": 2500.0, "bf16x3": 2500.0, "f16f8": 2500.0, "fp32": 157.3}
 # conv layer counts per network: (64->64 convs, stems, heads) — SURVEY.md §2 table
 LAYERS = {"DenoiseCNN": (18, 1, 1), "RRCDNet": (29, 2, 2), "DSDN": (32, 1, 1), "PIDN": (30, 1, 1),
           "ADSDN": (32, 1, 1), "APIDN": (30, 1, 1)}
@@ -94,7 +94,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--arch", default="RRCDNet")
-    ap.add_argument("--dtype", default="bf16x3", choices=["bf16", "bf16x3", "fp32"])
+    ap.add_argument("--dtype", default="bf16x3", choices=["bf16", "bf16x3", "f16f8", "fp32"])
     ap.add_argument("--batch", type=int, default=8192, help="spectra per GPU per step")
     ap.add_argument("--L", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=20250410)
@@ -158,7 +158,7 @@ def main():
 
     variants = {}
     if not args.no_variants:
-        for dt in ("bf16x3", "bf16", "fp32"):
+        for dt in ("f16f8", "bf16x3", "bf16", "fp32"):
             if dt == args.dtype:
                 continue
             nb = B if dt != "fp32" else max(1, B // 4)

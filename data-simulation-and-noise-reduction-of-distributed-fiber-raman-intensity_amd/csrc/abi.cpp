@@ -15,6 +15,8 @@ size_t packed_bytes(const std::vector<Op>& spec, int dtype);
 hipError_t launch_fused16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
 hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                 hipStream_t s);
+bool has_fused_h8(int arch);
+hipError_t launch_fused_h8(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
 hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                void* ws, size_t ws_bytes, hipStream_t s);
 size_t cbam_workspace_bytes(int arch, int dtype, int64_t n, int64_t L);
@@ -38,7 +40,7 @@ int hip_check(hipError_t e, const char* what) {
 }
 
 bool valid_arch(int a) { return a >= RDN_DENOISECNN && a <= RDN_APIDN; }
-bool valid_dtype(int d) { return d == RDN_F32 || d == RDN_BF16 || d == RDN_BF16X3; }
+bool valid_dtype(int d) { return d == RDN_F32 || d == RDN_BF16 || d == RDN_BF16X3 || d == RDN_F16F8; }
 bool is_cbam(int a) { return a == RDN_ADSDN || a == RDN_APIDN; }
 
 }  // namespace
@@ -119,12 +121,15 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
   const hipStream_t s = (hipStream_t)stream;
   const uint8_t* blob = (const uint8_t*)packed;
   if (is_cbam(arch)) {
+    if (dtype == RDN_F16F8) return fail(RDN_EUNSUPPORTED, "rdn_forward: RDN_F16F8 is not built for the CBAM networks");
     const size_t need = rdn::cbam_workspace_bytes(arch, dtype, n, L);
     if (ws_bytes < need || (need && !ws))
       return fail(RDN_ESIZE, "rdn_forward: workspace too small, need " + std::to_string(need) + " bytes");
     return hip_check(rdn::launch_cbam_forward(arch, dtype, blob, x, y, n, (int)L, ws, ws_bytes, s), "cbam forward");
   }
   if (dtype == RDN_BF16) return hip_check(rdn::launch_fused16(arch, blob, x, y, n, (int)L, s), "fused bf16 forward");
+  if (dtype == RDN_F16F8 && rdn::has_fused_h8(arch))
+    return hip_check(rdn::launch_fused_h8(arch, blob, x, y, n, (int)L, s), "fused f16f8 forward");
   return hip_check(rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, s), "fused in-place forward");
   RDN_GUARD_END
 }

@@ -42,6 +42,24 @@ constexpr int BIG_BYTES_BF16 = BIG_FRAG_BYTES_BF16 + C * 4;                // 24
 // map above and W = hi + lo; then bias[64] f32.
 constexpr int BIG_FRAG_FLOATS_F32 = 4 * 12 * 64 * 4;                       // 12288
 constexpr int BIG_BYTES_F32 = (BIG_FRAG_FLOATS_F32 + C) * 4;               // 49408
+// f16 + e4m3-correction big layer (RDN_F16F8, inplace.hpp Op<MODE_H8>):
+//   [m 4][kstep 6][lane 64][8 f16]   A-fragments of v_mfma_f32_16x16x32_f16 for W_hi = f16(W),
+//                                    K order h16_channel (as the bf16 layout below)
+//   [m 4][tap 3][lane 64][32 x e4m3] A-fragments of v_mfma_scale_f32_16x16x128_f8f6f4: lane
+//                                    r + 16g holds bytes [W_lo (16) | W_hi (16)] of cout 16m + r for
+//                                    the 16 channels of e4m3 activation bytes 16g .. 16g+15
+//   [m 4][lane 64] u32               E8M0 block scales, byte t = tap t (lane r + 16kb: block kb of
+//                                    row r: kb 0/1 = W_lo channels 0-31 / 32-63, kb 2/3 = W_hi)
+//   bias[64] f32
+constexpr int H8_MAIN_BYTES = 4 * 6 * 64 * 16;                             // 24576
+constexpr int H8_CORR_OFF = H8_MAIN_BYTES;
+constexpr int H8_SCALE_OFF = H8_CORR_OFF + 4 * 3 * 64 * 32;                // 49152
+constexpr int H8_BIAS_OFF = H8_SCALE_OFF + 4 * 64 * 4;                     // 50176
+constexpr int BIG_BYTES_H8 = H8_BIAS_OFF + C * 4;                          // 50432
+// activation planes: e4m3(hi / 4) and e4m3(lo * 2^9) (MFMA E8M0 block scales 127+2 / 127-9); with
+// activations saturated to +-1792 (= 448 * 4) neither conversion can leave the e4m3 range
+constexpr int H8_HI_E8M0 = 129, H8_LO_E8M0 = 118;
+constexpr float H8_HI_DIV = 4.0f, H8_LO_DIV = 1.0f / 512.0f, H8_SAT = 1792.0f;
 
 // 16-bit single-rounding layout of fused16.hip (RDN_BF16, non-CBAM networks): the same
 // [m 4][kstep 6][lane 64][8] fragments + bias, but with the K order permuted so that element j of
@@ -76,7 +94,7 @@ __device__ __forceinline__ uint32_t off_f32(int prow, int byte) {
 }
 
 enum Arch : int { DENOISECNN = 0, RRCDNET = 1, DSDN = 2, ADSDN = 3, PIDN = 4, APIDN = 5 };
-enum DType : int { F32 = 0, BF16 = 1, BF16X3 = 2 };
+enum DType : int { F32 = 0, BF16 = 1, BF16X3 = 2, F16F8 = 3 };
 
 // receptive half-width (rows of halo needed on each side of a tile's outputs)
 __host__ __device__ constexpr int fused_halo(int arch) {

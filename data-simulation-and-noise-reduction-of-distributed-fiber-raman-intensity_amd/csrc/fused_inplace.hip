@@ -1,5 +1,5 @@
 // Whole-network fused tile kernels on the in-place 256-byte-row tile (see inplace.hpp):
-// exact-fp32 (MODE_F32) and split-bf16 (MODE_X3) variants of 1DCNN, RRCDNet, DSDN and PIDN.
+// exact-fp32 (MODE_F32), split-bf16 (MODE_X3) and f16 + e4m3-correction (MODE_H8) variants of 1DCNN, RRCDNet, DSDN and PIDN.
 //
 // Reference forwards: 1DCNN/train.py:71-82, RRCDNet/train.py:72-98, DSDN/train.py:72-126,
 // PIDN/train.py:72-106.
@@ -133,26 +133,33 @@ IP_KERNEL(pidn, PIDN)
 
 typedef void (*fused_kernel_t)(const uint8_t*, const float*, float*, int, int, int);
 
-// dtype: F32 (exact fp32) or BF16X3 (split bf16); see common.hpp
+template <int MODE>
+static fused_kernel_t pick(int arch) {
+  switch (arch) {
+    case DENOISECNN: return ip::denoisecnn<MODE>;
+    case RRCDNET: return ip::rrcdnet<MODE>;
+    case DSDN: return ip::dsdn<MODE>;
+    case PIDN: return ip::pidn<MODE>;
+    default: return nullptr;
+  }
+}
+
+// dtype: F32 (exact fp32), BF16X3 (split bf16) or F16F8 (f16 + e4m3 correction); see common.hpp
 hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                 hipStream_t stream) {
-  fused_kernel_t k = nullptr;
-  const bool x3 = dtype == BF16X3;
-  switch (arch) {
-    case DENOISECNN: k = x3 ? ip::denoisecnn<ip::MODE_X3> : ip::denoisecnn<ip::MODE_F32>; break;
-    case RRCDNET: k = x3 ? ip::rrcdnet<ip::MODE_X3> : ip::rrcdnet<ip::MODE_F32>; break;
-    case DSDN: k = x3 ? ip::dsdn<ip::MODE_X3> : ip::dsdn<ip::MODE_F32>; break;
-    case PIDN: k = x3 ? ip::pidn<ip::MODE_X3> : ip::pidn<ip::MODE_F32>; break;
-    default: return hipErrorInvalidValue;
-  }
+  if (arch < 0 || arch >= 8 || dtype < 0 || dtype >= 4) return hipErrorInvalidValue;
+  const fused_kernel_t k = dtype == BF16X3 ? pick<ip::MODE_X3>(arch)
+                           : dtype == F16F8 ? pick<ip::MODE_H8>(arch)
+                           : dtype == F32   ? pick<ip::MODE_F32>(arch) : nullptr;
+  if (!k) return hipErrorInvalidValue;
   const int nbk = arch == DSDN ? ip::NetGeo<DSDN>::NBK : ip::NetGeo<RRCDNET>::NBK;
   const int wb = 128 * nbk;
   const uint32_t lds = nbk == 4 ? ip::TileGeo<4>::LDS : ip::TileGeo<5>::LDS;
-  static bool attr_set[2][8] = {};
-  if (!attr_set[x3][arch]) {
+  static bool attr_set[4][8] = {};
+  if (!attr_set[dtype][arch]) {
     const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    attr_set[x3][arch] = true;
+    attr_set[dtype][arch] = true;
   }
   const int H = fused_halo(arch), T = wb - 2 * H, tiles = (L + T - 1) / T;
   const int64_t chunk = (int64_t)(0x7fffffff / tiles);

@@ -23,7 +23,7 @@
 namespace rdn {
 namespace ip {
 
-constexpr int MODE_F32 = 0, MODE_B1 = 1, MODE_X3 = 2;
+constexpr int MODE_F32 = 0, MODE_B1 = 1, MODE_X3 = 2, MODE_H8 = 3;
 #ifndef RDN_IP_SPREAD_STORE
 #define RDN_IP_SPREAD_STORE 1
 #endif
@@ -44,8 +44,11 @@ template <int NBK> struct TileGeo {
 };
 static_assert(TileGeo<4>::LDS == LDS_BYTES, "CBAM geometry");
 static_assert(TileGeo<5>::LDS == 163840, "fused geometry fills the LDS");
-constexpr int BIG_BYTES = BIG_BYTES_F32;                         // both modes: 49408 B per layer
-constexpr int BIAS_OFF = BIG_FRAG_FLOATS_F32 * 4;                // 49152
+// bytes per packed big layer and offset of its bias: f32 / split-bf16 / bf16 49408 (bias at 49152),
+// f16 + e4m3 correction 50432 (bias at 50176)
+template <int MODE> struct LayerBytes {
+  static constexpr int BYTES = BIG_BYTES_F32, BIAS = BIG_FRAG_FLOATS_F32 * 4;
+};
 
 enum Epi : int { RELU = 1, ADD_ID = 2, SAVE_ID = 4 };
 
@@ -97,7 +100,7 @@ template <> struct Op<MODE_F32> {
   __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v) {
     *(f32x4*)(act + ad[0] + off) = v;
   }
-  __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc) {
+  __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc, uint32_t, int) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w[i], b.v[i], acc, 0, 0, 0);
     return acc;
@@ -141,7 +144,7 @@ template <> struct Op<MODE_X3> {
     *(bf16x4*)(act + ad[0] + off) = hi;
     *(bf16x4*)(act + ad[1] + off) = lo;
   }
-  __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc) {
+  __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc, uint32_t, int) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo, b.hi, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, acc, 0, 0, 0);
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, acc, 0, 0, 0);
@@ -180,7 +183,7 @@ template <> struct Op<MODE_B1> {
   __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v) {
     *(bf16x4*)(act + ad[0] + off) = __builtin_convertvector(v, bf16x4);
   }
-  __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc) {
+  __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc, uint32_t, int) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, acc, 0, 0, 0);
   }
   __device__ static void store4(char* act, int prow, int c0, f32x4 v) {
@@ -188,6 +191,114 @@ template <> struct Op<MODE_B1> {
   }
   __device__ static f32x4 load4(const char* act, int prow, int c0) {
     return __builtin_convertvector(*(const bf16x4*)(act + off_f32(prow, 2 * c0)), f32x4);
+  }
+};
+
+// f16 main product + block-scaled e4m3 correction (RDN_F16F8).  Row = [hi: 64 ch f16 (128 B) |
+// e4m3(hi / 4) (64 B) | e4m3(lo * 2^9) (64 B)], v = hi + lo, channels in h16_channel order within
+// each plane (the 8 outputs of lane quarter q of an M-tile pair {2u, 2u+1} are 16-B f16 slot 4u+q
+// and 8-B e4m3 slot 4u+q).  One k-step per tap:
+//   W.X ~= W_hi.X_hi (2 x v_mfma_f32_16x16x32_f16, K = 64)
+//        + [W_lo | W_hi] . [X_hi | X_lo]  (1 x v_mfma_scale_f32_16x16x128_f8f6f4, e4m3, K = 128),
+// i.e. the two correction products of the split-bf16 mode in ONE fp8 MFMA at 2x the 16-bit rate:
+// 64 MFMA cycles per (tap, 16 x 16 tile) instead of 96.  W_lo/W_hi e4m3 carry per-32-channel E8M0
+// scales (packed on the host); the activation planes use fixed scales (common.hpp H8_*), and the
+// stored activation saturates at +-1792 so that no conversion leaves the e4m3 range
+// (v_cvt_*_fp8 returns NaN there).  CPU emulation on trained RRCDNet (tools/precision_sweep.py):
+// 1.5e-3 max-abs, vs 0.030 for plain f16 and 0.20 for plain bf16.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+// 4 floats -> 4 e4m3 bytes of v / div (v_cvt_scalef32_pk_fp8_f32: the division is free)
+__device__ __forceinline__ uint32_t pk_e4m3_div(f32x4 v, float div) {
+  s16x2 o = {0, 0};
+  o = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(o, v[0], v[1], div, false);
+  o = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(o, v[2], v[3], div, true);
+  return __builtin_bit_cast(uint32_t, o);
+}
+__device__ __forceinline__ f32x4 unpk_e4m3(uint32_t w) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, false), b = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, true);
+  return f32x4{a[0], a[1], b[0], b[1]};
+}
+// saturate (and, with RELU, rectify) in one v_med3 per value
+template <bool RELU>
+__device__ __forceinline__ f32x4 h8_sat(f32x4 v) {
+  const float lo = RELU ? 0.f : -H8_SAT;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_fmed3f(v[i], lo, H8_SAT);
+  return v;
+}
+// split a saturated activation into its three plane encodings
+struct H8Split {
+  f16x4 hi;
+  uint32_t hi8, lo8;
+};
+__device__ __forceinline__ H8Split h8_split(f32x4 r) {
+  const f16x4 h = __builtin_convertvector(r, f16x4);
+  const f32x4 g = __builtin_convertvector(h, f32x4);
+  return H8Split{h, pk_e4m3_div(g, H8_HI_DIV), pk_e4m3_div(r - g, H8_LO_DIV)};
+}
+
+template <> struct LayerBytes<MODE_H8> {
+  static constexpr int BYTES = BIG_BYTES_H8, BIAS = H8_BIAS_OFF;
+};
+
+template <> struct Op<MODE_H8> {
+  static constexpr int KSTEPS = 3;
+  struct A { f16x8 h[2]; i32x8 c; };
+  struct B { f16x8 h[2]; i32x8 c; };
+  __device__ static A load_a(const uint8_t* layer, int m, int s, int lane) {
+    const f16x8* f = (const f16x8*)layer + (m * 6 + 2 * s) * 64 + lane;
+    return A{{f[0], f[64]}, *(const i32x8*)(layer + H8_CORR_OFF + ((m * 3 + s) * 64 + lane) * 32)};
+  }
+  __device__ static int tap(int s) { return s; }
+  static constexpr int PLANES = 4;
+  // B fragment of k-step s: f16 slots q (channels 0-31) and 4+q (32-63), e4m3 hi / lo bytes 16q..16q+15
+  __device__ static int bslot(int, int q, int p) { return 4 * p + q; }
+  // stores: byte of channels [c0, c0+4) in plane p (0 f16, 1 e4m3 hi, 2 e4m3 lo)
+  __device__ static int sbyte(int c0, int p) {
+    const int mt = c0 >> 4, slot = 4 * (mt >> 1) + ((c0 >> 2) & 3), half = mt & 1;
+    return p == 0 ? 16 * slot + 8 * half : (p == 1 ? 128 : 192) + 8 * slot + 4 * half;
+  }
+  __device__ static B load_b_at(const char* act, const uint32_t (&ad)[PLANES], uint32_t off) {
+    const i32x4v ch = *(const i32x4v*)(act + ad[2] + off), cl = *(const i32x4v*)(act + ad[3] + off);
+    return B{{*(const f16x8*)(act + ad[0] + off), *(const f16x8*)(act + ad[1] + off)},
+             __builtin_shufflevector(ch, cl, 0, 1, 2, 3, 4, 5, 6, 7)};
+  }
+  __device__ static B load_b(const char* act, int prow, int s, int q) {
+    uint32_t ad[PLANES];
+#pragma unroll
+    for (int p = 0; p < PLANES; ++p) ad[p] = off_f32(prow, 16 * bslot(s, q, p));
+    return load_b_at(act, ad, 0);
+  }
+  __device__ static void put(char* act, uint32_t a0, uint32_t a1, uint32_t a2, f32x4 v) {
+    const H8Split x = h8_split(h8_sat<false>(v));
+    *(f16x4*)(act + a0) = x.hi;
+    *(uint32_t*)(act + a1) = x.hi8;
+    *(uint32_t*)(act + a2) = x.lo8;
+  }
+  __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v) {
+    put(act, ad[0] + off, ad[1] + off, ad[2] + off, v);
+  }
+  __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc, uint32_t sa, int s) {
+    const int sb = (threadIdx.x & 32) ? H8_LO_E8M0 : H8_HI_E8M0;   // lanes 32-63: the lo blocks
+    if (s == 0) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 0, (int)sa, 0, sb);
+    else if (s == 1) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 1, (int)sa, 0, sb);
+    else acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 2, (int)sa, 0, sb);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[0], b.h[0], acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[1], b.h[1], acc, 0, 0, 0);
+  }
+  __device__ static void store4(char* act, int prow, int c0, f32x4 v) {
+    put(act, off_f32(prow, sbyte(c0, 0)), off_f32(prow, sbyte(c0, 1)), off_f32(prow, sbyte(c0, 2)), v);
+  }
+  __device__ static f32x4 load4(const char* act, int prow, int c0) {
+    const f16x4 h = *(const f16x4*)(act + off_f32(prow, sbyte(c0, 0)));
+    const uint32_t l = *(const uint32_t*)(act + off_f32(prow, sbyte(c0, 2)));
+    return __builtin_convertvector(h, f32x4) + unpk_e4m3(l) * H8_LO_DIV;
   }
 };
 
@@ -284,20 +395,27 @@ template <int MODE>
 struct LayerA {
   typename Op<MODE>::A v[IP_MT][Op<MODE>::KSTEPS];
   f32x4 bias[IP_MT];           // lane quarter q's 4 output channels of each M-tile (accumulator init)
+  uint32_t sc[IP_MT];          // MODE_H8: E8M0 scales of the correction fragments (byte t = tap t)
   __device__ __forceinline__ typename Op<MODE>::A (&operator[](int mm))[Op<MODE>::KSTEPS] { return v[mm]; }
 };
 
+template <int MODE>
 __device__ __forceinline__ f32x4 load_bias(const uint8_t* wl, int m) {
-  return *(const f32x4*)(wl + BIAS_OFF + (16 * m + 4 * ((threadIdx.x & 63) >> 4)) * 4);
+  return *(const f32x4*)(wl + LayerBytes<MODE>::BIAS + (16 * m + 4 * ((threadIdx.x & 63) >> 4)) * 4);
+}
+template <int MODE>
+__device__ __forceinline__ uint32_t load_scale(const uint8_t* wl, int m) {
+  return MODE == MODE_H8 ? ((const uint32_t*)(wl + H8_SCALE_OFF))[m * 64 + (threadIdx.x & 63)] : 0u;
 }
 
 template <int MODE>
 __device__ __forceinline__ void load_layer_a(const Tile& tl, int layer, LayerA<MODE>& a) {
   const int tid = opaque_tid(), mp = (tid >> 6) & 1, lane = tid & 63;
-  const uint8_t* wl = tl.big + (size_t)layer * BIG_BYTES;
+  const uint8_t* wl = tl.big + (size_t)layer * LayerBytes<MODE>::BYTES;
 #pragma unroll
   for (int mm = 0; mm < IP_MT; ++mm) {
-    a.bias[mm] = load_bias(wl, IP_MT * mp + mm);
+    a.bias[mm] = load_bias<MODE>(wl, IP_MT * mp + mm);
+    a.sc[mm] = load_scale<MODE>(wl, IP_MT * mp + mm);
 #pragma unroll
     for (int s = 0; s < Op<MODE>::KSTEPS; ++s) a[mm][s] = Op<MODE>::load_a(wl, IP_MT * mp + mm, s, lane);
   }
@@ -322,14 +440,15 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   const int lane = tid & 63, w = tid >> 6;
   const int mp = w & 1, nq = w >> 1;
   const int q = lane >> 4, c16 = lane & 15;
-  const uint8_t* wcur = tl.big + (size_t)tl.layer * BIG_BYTES;
-  const uint8_t* wnext = wcur + BIG_BYTES;
+  const uint8_t* wcur = tl.big + (size_t)tl.layer * LayerBytes<MODE>::BYTES;
+  const uint8_t* wnext = wcur + LayerBytes<MODE>::BYTES;
   // bf16 modes start the accumulators at the folded bias; exact fp32 keeps the reference's
   // order (sum of products, then + bias) for its 1e-5 parity
   constexpr bool BIAS_INIT = MODE != MODE_F32;
   f32x4 bias_l[MT];
+  uint32_t sc_l[MT];
 #pragma unroll
-  for (int mm = 0; mm < MT; ++mm) bias_l[mm] = a.bias[mm];
+  for (int mm = 0; mm < MT; ++mm) bias_l[mm] = a.bias[mm], sc_l[mm] = a.sc[mm];
 
   // LDS byte addresses of this lane's B fragments for every k-step (row = first row of the wave's
   // share of block 0), and of its output stores; blocks and N-tiles add multiples of 16 rows,
@@ -412,7 +531,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
           part[k][i][mm] = k == 0 && BIAS_INIT ? a.bias[mm] : f32x4{0.f, 0.f, 0.f, 0.f};
     if (j == NB - 1 && has_next) {                    // last use of this layer's bias
 #pragma unroll
-      for (int mm = 0; mm < MT; ++mm) a.bias[mm] = load_bias(wnext, MT * mp + mm);
+      for (int mm = 0; mm < MT; ++mm) a.bias[mm] = load_bias<MODE>(wnext, MT * mp + mm), a.sc[mm] = load_scale<MODE>(wnext, MT * mp + mm);
     }
 #pragma unroll
     for (int s = 0; s < O::KSTEPS; ++s) {
@@ -438,7 +557,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #if defined(RDN_ABLATE_NOMFMA)
           part[s % S][i][mm] += *(const f32x4*)&b;
 #else
-          part[s % S][i][mm] = O::mma(a[mm][s], b, part[s % S][i][mm]);
+          part[s % S][i][mm] = O::mma(a[mm][s], b, part[s % S][i][mm], sc_l[mm], s);
 #endif
         }
       }
@@ -449,7 +568,16 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #if RDN_IP_SPREAD_STORE
       // lagged write-back of block j-2, one (N-tile, M-tile) piece per k-step: the LDS write
       // bursts of the 8 waves spread over the block instead of landing on its first k-step
-      if (j >= 2 && s < NT * MT) store_piece(j - 2, s / MT, s % MT);
+      // (NT * MT = 4 pieces over KSTEPS = 3 (MODE_H8), 6 or 12 k-steps)
+      if (j >= 2) {
+        constexpr int NP = NT * MT;
+        if constexpr (O::KSTEPS >= NP) {
+          if (s < NP) store_piece(j - 2, s / MT, s % MT);
+        } else {
+#pragma unroll
+          for (int pc = s * NP / O::KSTEPS; pc < (s + 1) * NP / O::KSTEPS; ++pc) store_piece(j - 2, pc / MT, pc % MT);
+        }
+      }
 #else
       if (s == 0 && j >= 2) store_block(j - 2);                        // lagged write-back
 #endif

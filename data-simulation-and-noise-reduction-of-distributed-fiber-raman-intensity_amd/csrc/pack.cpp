@@ -131,6 +131,7 @@ static bool has_cbam(const std::vector<Op>& spec) {
 }
 int big_layout(const std::vector<Op>& spec, int dtype) {
   if (dtype == F32) return F32;
+  if (dtype == F16F8) return F16F8;
   if (dtype == BF16 && !has_cbam(spec)) return BF16;
   return BF16X3;
 }
@@ -246,6 +247,94 @@ static void pack_big_x3(const Folded& f, uint8_t* dst) {
   for (int c = 0; c < C; ++c) bias[c] = (float)f.b[c];
 }
 
+// ---- f16 + e4m3 correction layout (common.hpp BIG_BYTES_H8, inplace.hpp Op<MODE_H8>) --------------
+
+// OCP e4m3fn (bias 7, max 448, subnormal step 2^-9), round to nearest even, saturating
+static uint8_t to_e4m3(double v) {
+  const uint8_t sign = v < 0 ? 0x80 : 0;
+  double a = std::fabs(v);
+  if (!(a > 0)) return sign;
+  if (a >= 448.0) return sign | 0x7e;
+  int e;
+  std::frexp(a, &e);                      // a = f * 2^e, f in [0.5, 1)
+  e -= 1;                                 // a in [2^e, 2^(e+1))
+  if (e < -6) e = -6;                     // subnormal range shares the step of [2^-6, 2^-5)
+  const double step = std::ldexp(1.0, e - 3);
+  double q = std::nearbyint(a / step);    // default rounding mode: nearest even
+  double r = q * step;
+  if (r >= 448.0) return sign | 0x7e;
+  // re-encode r exactly
+  if (r < std::ldexp(1.0, -6)) return sign | (uint8_t)std::lround(r / std::ldexp(1.0, -9));
+  int er;
+  const double fr = std::frexp(r, &er);   // r = fr * 2^er
+  const int E = er - 1 + 7;
+  const int M = (int)std::lround((fr * 2.0 - 1.0) * 8.0);
+  return sign | (uint8_t)((E << 3) | M);
+}
+
+// E8M0 block scale so that the block's largest magnitude lands in (224, 448]
+static int e8m0_for(double amax) {
+  if (!(amax > 0)) return 127;
+  int e = (int)std::ceil(std::log2(amax / 448.0));
+  while (std::ldexp(amax, -e) > 448.0) ++e;
+  while (e > -127 && std::ldexp(amax, -(e - 1)) <= 448.0) --e;
+  return e + 127 < 0 ? 0 : (e + 127 > 254 ? 254 : e + 127);
+}
+
+static void pack_big_h8(const Folded& f, uint8_t* dst) {
+  _Float16* main = (_Float16*)dst;
+  // hi / lo split of every weight: hi = f16(fp32(W)), lo = W - hi (fp64)
+  std::vector<double> hi((size_t)C * C * 3), lo((size_t)C * C * 3);
+  for (int co = 0; co < C; ++co)
+    for (int ci = 0; ci < C; ++ci)
+      for (int t = 0; t < 3; ++t) {
+        const double w = co < f.cout ? f.W(co, ci, t) : 0.0;
+        const double h = (double)(_Float16)(float)w;
+        hi[((size_t)co * C + ci) * 3 + t] = h;
+        lo[((size_t)co * C + ci) * 3 + t] = w - h;
+      }
+  auto H = [&](int co, int ci, int t) { return hi[((size_t)co * C + ci) * 3 + t]; };
+  auto Lo = [&](int co, int ci, int t) { return lo[((size_t)co * C + ci) * 3 + t]; };
+  for (int m = 0; m < 4; ++m)
+    for (int s = 0; s < 6; ++s)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int t = s >> 1, u = s & 1;
+          const int co = 16 * m + (lane & 15), ci = h16_channel(4 * u + (lane >> 4), j);
+          main[(((m * 6 + s) * 64) + lane) * 8 + j] = (_Float16)H(co, ci, t);
+        }
+  // e4m3 activation byte b of a plane holds channel h16_channel(b >> 3, b & 7); blocks of 32 bytes
+  // = channels [0, 32) and [32, 64)
+  auto chan = [](int b) { return h16_channel(b >> 3, b & 7); };
+  uint8_t* corr = dst + H8_CORR_OFF;
+  uint32_t* scales = (uint32_t*)(dst + H8_SCALE_OFF);
+  for (int m = 0; m < 4; ++m)
+    for (int r = 0; r < 16; ++r) {
+      const int co = 16 * m + r;
+      for (int t = 0; t < 3; ++t) {
+        int sc[4];                     // kb 0/1: lo channels 0-31 / 32-63; kb 2/3: hi
+        for (int kb = 0; kb < 4; ++kb) {
+          double amax = 0;
+          for (int b = 32 * (kb & 1); b < 32 * (kb & 1) + 32; ++b)
+            amax = std::fmax(amax, std::fabs(kb < 2 ? Lo(co, chan(b), t) : H(co, chan(b), t)));
+          sc[kb] = e8m0_for(amax);
+          uint32_t& word = scales[m * 64 + r + 16 * kb];
+          word = (word & ~(0xffu << (8 * t))) | ((uint32_t)sc[kb] << (8 * t));
+        }
+        for (int g = 0; g < 4; ++g) {
+          uint8_t* lanebytes = corr + ((m * 3 + t) * 64 + r + 16 * g) * 32;
+          for (int jj = 0; jj < 16; ++jj) {
+            const int b = 16 * g + jj, ci = chan(b), kb = b >> 5;
+            lanebytes[jj] = to_e4m3(std::ldexp(Lo(co, ci, t), -(sc[kb] - 127)));
+            lanebytes[16 + jj] = to_e4m3(std::ldexp(H(co, ci, t), -(sc[2 + kb] - 127)));
+          }
+        }
+      }
+    }
+  float* bias = (float*)(dst + H8_BIAS_OFF);
+  for (int c = 0; c < C; ++c) bias[c] = c < f.cout ? (float)f.b[c] : 0.f;
+}
+
 static void pack_small_conv(const Folded& f, float* slot) {   // w[c*3+t], bias at 192 (+c)
   std::memset(slot, 0, SMALL_SLOT_FLOATS * sizeof(float));
   if (f.cin == 1) {
@@ -290,8 +379,12 @@ static bool pack_cbam(Reader& rd, const Op& o, float* small) {
   return true;
 }
 
+static size_t layer_bytes(int layout) {
+  return layout == BF16 ? BIG_BYTES_BF16 : layout == F16F8 ? BIG_BYTES_H8 : BIG_BYTES_F32;
+}
+
 size_t packed_bytes(const std::vector<Op>& spec, int dtype) {
-  return SMALL_BYTES + (size_t)big_layers(spec, dtype) * (big_layout(spec, dtype) == BF16 ? BIG_BYTES_BF16 : BIG_BYTES_F32);
+  return SMALL_BYTES + (size_t)big_layers(spec, dtype) * layer_bytes(big_layout(spec, dtype));
 }
 
 
@@ -300,7 +393,7 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
                  size_t cap) {
   const std::vector<Op> spec = net_spec(arch);
   if (spec.empty()) return "unknown arch " + std::to_string(arch);
-  if (dtype != F32 && dtype != BF16 && dtype != BF16X3) return "unknown dtype " + std::to_string(dtype);
+  if (dtype != F32 && dtype != BF16 && dtype != BF16X3 && dtype != F16F8) return "unknown dtype " + std::to_string(dtype);
   const size_t need = packed_bytes(spec, dtype);
   if (cap < need) return "destination too small: need " + std::to_string(need) + " bytes";
   uint8_t* out = (uint8_t*)dst;
@@ -308,7 +401,7 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
   float* small = (float*)out;
   uint8_t* big = out + SMALL_BYTES;
   const int layout = big_layout(spec, dtype);
-  const size_t big_bytes = layout == BF16 ? BIG_BYTES_BF16 : BIG_BYTES_F32;
+  const size_t big_bytes = layer_bytes(layout);
   Reader rd{tensors, numels, n};
   int layer = 0;
   for (const Op& o : spec) {
@@ -322,6 +415,7 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
         if (!fold(rd, o, C, C, f)) return rd.err;
         if (layout == BF16) pack_big_bf16(f, big + layer * big_bytes);
         else if (layout == BF16X3) pack_big_x3(f, big + layer * big_bytes);
+        else if (layout == F16F8) pack_big_h8(f, big + layer * big_bytes);
         else pack_big_f32(f, big + layer * big_bytes);
         ++layer;
         break;

@@ -12,7 +12,7 @@ from . import _lib
 
 ARCHS = ("DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN")
 ARCH_ID = {a: i for i, a in enumerate(ARCHS)}
-DTYPE_ID = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "bf16x3": 2}
+DTYPE_ID = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1, "bf16x3": 2, "f16f8": 3}
 
 
 def _arch(arch):
@@ -30,7 +30,7 @@ def _dtype(dtype):
     try:
         return DTYPE_ID[dtype]
     except KeyError:
-        raise ValueError(f"unknown engine dtype {dtype!r}; expected 'fp32' or 'bf16'") from None
+        raise ValueError(f"unknown engine dtype {dtype!r}; expected one of 'fp32', 'bf16', 'bf16x3', 'f16f8'") from None
 
 
 def _stream(device):

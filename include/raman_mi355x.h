@@ -48,8 +48,13 @@ typedef enum {
  *   RDN_F32    exact-fp32 MFMA, fp32 activations               (1e-5 parity mode)
  *   RDN_BF16   one bf16 MFMA per product, bf16 activations      (fastest)
  *   RDN_BF16X3 split bf16: operands as bf16 hi+lo pairs, three bf16 MFMAs per product
- *              (hi*hi + hi*lo + lo*hi), ~16-bit operands        (bf16 MFMA at 2e-2-safe accuracy) */
-typedef enum { RDN_F32 = 0, RDN_BF16 = 1, RDN_BF16X3 = 2 } rdn_dtype;
+ *              (hi*hi + hi*lo + lo*hi), ~16-bit operands        (bf16 MFMA at 2e-2-safe accuracy)
+ *   RDN_F16F8  f16 main product (v = hi + lo, hi = f16(v)) plus both correction products
+ *              W_lo*X_hi + W_hi*X_lo as ONE block-scaled e4m3 MFMA at twice the 16-bit rate; f16 hi
+ *              + e4m3 lo activations (~15 significant bits).  2e-2-safe at 2/3 of the MFMA cycles
+ *              of RDN_BF16X3.  Non-CBAM networks only (CBAM networks: RDN_EUNSUPPORTED);
+ *              activations must stay below the f16 range (65504). */
+typedef enum { RDN_F32 = 0, RDN_BF16 = 1, RDN_BF16X3 = 2, RDN_F16F8 = 3 } rdn_dtype;
 
 enum {
   RDN_OK = 0,

@@ -150,3 +150,49 @@ def test_bn_folding_matches_reference_math():
     y = torch.nn.functional.batch_norm(y, sd["right_net.5.1.running_mean"].double(), sd["right_net.5.1.running_var"].double(),
                                        sd["right_net.5.1.weight"].double(), sd["right_net.5.1.bias"].double(), False, 0, 1e-5)
     assert (y_fold - y).abs().max() / y.abs().max() < 1e-6
+
+
+def test_pack_layout_f16f8():
+    """RDN_F16F8 layer (common.hpp BIG_BYTES_H8): f16 hi fragments, e4m3 [lo | hi] correction fragments
+    with per-(row, 32-channel block, tap) E8M0 scales; hi + lo reproduces the folded weight to ~2^-15."""
+    from raman_mi355x import engine
+    sd = golden_state_dict("RRCDNet", "trained")
+    blob = engine.pack("RRCDNet", sd, "f16f8", "cpu").numpy()
+    assert blob.size == engine.packed_size("RRCDNet", "f16f8") == SMALL + 29 * 50432
+    w, b = _fold(sd, "left_net.3.0", None)          # big layer 15
+    w64 = _fold_f64(sd, "left_net.3.0")
+    L = blob[SMALL + 15 * 50432:SMALL + 16 * 50432]
+    lane = np.arange(64)
+    main = L[:24576].view(np.float16).reshape(4, 6, 64, 8)
+    corr = L[24576:49152].reshape(4, 3, 64, 32)
+    scales = L[49152:50176].view(np.uint32).reshape(4, 64)
+    np.testing.assert_array_equal(L[50176:].view(np.float32), b)
+    e4m3 = torch.from_numpy(corr.copy()).view(torch.float8_e4m3fn).float().numpy().astype(np.float64)
+    chan = lambda byte: 32 * ((byte >> 3) >> 2) + 4 * ((byte >> 3) & 3) + (byte & 7 & 3) + 16 * ((byte & 7) >> 2)
+    hi_full = np.zeros((64, 64, 3))
+    lo_full = np.zeros((64, 64, 3))
+    for m in range(4):
+        for s in range(6):
+            t, u = s >> 1, s & 1
+            for j in range(8):
+                cin = 32 * u + 4 * (lane >> 4) + (j & 3) + 16 * (j >> 2)
+                hi_full[16 * m + (lane & 15), cin, t] = main[m, s, :, j]
+        for t in range(3):
+            for ln in range(64):
+                r, g = ln & 15, ln >> 4
+                for jj in range(16):
+                    byte = 16 * g + jj
+                    kb = byte >> 5
+                    s_lo = float(2.0 ** (int((scales[m, r + 16 * kb] >> (8 * t)) & 0xFF) - 127))
+                    s_hi = float(2.0 ** (int((scales[m, r + 16 * (2 + kb)] >> (8 * t)) & 0xFF) - 127))
+                    co, ci = 16 * m + r, chan(byte)
+                    lo_full[co, ci, t] = e4m3[m, t, ln, jj] * s_lo
+                    # the e4m3 copy of hi is within 2^-4 relative of the f16 hi
+                    assert abs(e4m3[m, t, ln, 16 + jj] * s_hi - hi_full[co, ci, t]) <= 2.0 ** -4 * abs(hi_full[co, ci, t]) + 1e-12
+    np.testing.assert_array_equal(hi_full.astype(np.float16), w.astype(np.float16))
+    err = np.abs(hi_full + lo_full - w64)
+    assert err.max() <= 2.0 ** -14 * np.abs(w64).max(), err.max()
+
+
+def _fold_f64(sd, conv):
+    return sd[conv + ".weight"].double().numpy()

@@ -60,7 +60,7 @@ def fold(sd, conv, bn):
 
 
 def rrcdnet(sd, x, mode):
-    wfmt, xfmt, wt, xt = mode
+    wfmt, xfmt, wt, xt = mode if mode else (None,)*4
     x = x.double()
 
     def big(h, conv, bn, dil, relu=True):

@@ -34,7 +34,7 @@ def main():
     for arch in args.archs:
         for L in ([10000, 16384] if arch in ("PIDN", "APIDN") else [10000]):
             for dt in args.dtypes:
-                B = {"bf16": 4096, "bf16x3": 2048, "fp32": 1024}[dt]
+                B = {"bf16": 4096, "bf16x3": 2048, "f16f8": 2048, "fp32": 1024}[dt]
                 if arch in ("ADSDN", "APIDN"):
                     B //= 2
                 B = max(64, B * 10000 // L)
