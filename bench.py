@@ -1,10 +1,13 @@
 """Headline benchmark: denoised spectra/s of the fused RRCDNet forward on MI355X (BASELINE.json).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--arch RRCDNet] [--dtype bf16x3] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--arch RRCDNet] [--dtype f16f8] [--batch B]
 
-The headline dtype is bf16x3: bf16 MFMA arithmetic with split (hi + lo) operands, the engine's bf16
-mode that meets the north-star bf16 tolerance (2e-2 max-abs) on trained weights.  Plain single-
-rounding bf16 and exact fp32 are timed as "variants" in the same line.
+The headline dtype is f16f8: the engine's fastest 16-bit mode that meets the north-star bf16
+tolerance (2e-2 max-abs) on trained weights.  Each product is an f16 MFMA on the f16-rounded
+operands plus ONE block-scaled e4m3 MFMA carrying both correction terms (W_lo.X_hi + W_hi.X_lo) at
+twice the 16-bit rate: 2 bf16-MFMA-equivalents per product.  The split-bf16 mode (bf16x3, 3 bf16
+MFMAs per product), plain single-rounding bf16 (fastest, NOT within 2e-2 on trained RRCDNet) and
+exact fp32 are timed as "variants" in the same line.
 
 One step = one forward of the fused network over a batch of B synthetic spectra per GPU (L = 10000),
 generated on-device by the engine's simulator BEFORE the timed region (inputs resident in HBM).
@@ -33,6 +36,8 @@ PEAK_TFLOPS = {"bf16": 2500.0, "bf16x3": 2500.0, "f16f8": 2500.0, "fp32": 157.3}
 LAYERS = {"DenoiseCNN": (18, 1, 1), "RRCDNet": (29, 2, 2), "DSDN": (32, 1, 1), "PIDN": (30, 1, 1),
           "ADSDN": (32, 1, 1), "APIDN": (30, 1, 1)}
 SA_CONVS = {"ADSDN": 17, "APIDN": 15}
+# MFMA cycles per product relative to one bf16 MFMA (v_mfma_f32_16x16x32_bf16 = 16 cycles per K=32)
+MFMA_COST = {"bf16": 1, "bf16x3": 3, "f16f8": 2}
 
 
 def flops_per_spectrum(arch, L):
@@ -94,7 +99,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--arch", default="RRCDNet")
-    ap.add_argument("--dtype", default="bf16x3", choices=["bf16", "bf16x3", "f16f8", "fp32"])
+    ap.add_argument("--dtype", default="f16f8", choices=["bf16", "bf16x3", "f16f8", "fp32"])
     ap.add_argument("--batch", type=int, default=8192, help="spectra per GPU per step")
     ap.add_argument("--L", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=20250410)
@@ -187,7 +192,8 @@ def main():
                          "frac": achieved / peak, "traffic": tps * B if tps else None,
                          "traffic_source": tsrc, "algorithmic_bytes": 8 * L * B,
                          "kernel_ms": kernel_ms, "flops_per_launch": fl,
-                         "mfma_products_per_flop": 3 if args.dtype == "bf16x3" else 1},
+                         "mfma_cost_per_product_bf16_units": MFMA_COST.get(args.dtype),
+                         "executed_bf16_equiv_tflops": achieved * MFMA_COST[args.dtype] if args.dtype in MFMA_COST else None},
             "variants": variants,
             "metrics_mean": {k: sums[i] / sums[4] for i, k in enumerate(["MSE", "SSIM", "Smoothness", "Peak2Peak"])},
         }

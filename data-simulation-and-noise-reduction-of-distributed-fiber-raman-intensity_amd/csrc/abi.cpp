@@ -15,8 +15,7 @@ size_t packed_bytes(const std::vector<Op>& spec, int dtype);
 hipError_t launch_fused16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
 hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                 hipStream_t s);
-bool has_fused_h8(int arch);
-hipError_t launch_fused_h8(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
+
 hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                void* ws, size_t ws_bytes, hipStream_t s);
 size_t cbam_workspace_bytes(int arch, int dtype, int64_t n, int64_t L);
@@ -128,8 +127,6 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
     return hip_check(rdn::launch_cbam_forward(arch, dtype, blob, x, y, n, (int)L, ws, ws_bytes, s), "cbam forward");
   }
   if (dtype == RDN_BF16) return hip_check(rdn::launch_fused16(arch, blob, x, y, n, (int)L, s), "fused bf16 forward");
-  if (dtype == RDN_F16F8 && rdn::has_fused_h8(arch))
-    return hip_check(rdn::launch_fused_h8(arch, blob, x, y, n, (int)L, s), "fused f16f8 forward");
   return hip_check(rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, s), "fused in-place forward");
   RDN_GUARD_END
 }

@@ -73,7 +73,7 @@ __device__ void prologue_cbam(Tile& tl, const Seg& sg, int n) {
   float* sa = (float*)(lds + SA_OFF);
   float* ca = (float*)(lds + CA_OFF);
   float* h1 = (float*)(lds + H1_OFF);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = __builtin_amdgcn_workitem_id_x(), lane = tid & 63, w = tid >> 6;
   const float* cw = tl.small + sg.cbam_slot * SMALL_SLOT_FLOATS;   // fc.0.weight [4][64]
   const float* cw2 = cw + SMALL_SLOT_FLOATS;                       // fc.2.weight [64][4]
   const float* cmisc = cw2 + SMALL_SLOT_FLOATS;                    // fc.0.bias[4], fc.2.bias[64], sa.w[2][7], sa.b
@@ -445,7 +445,7 @@ __device__ __forceinline__ void publish_stats(const Tile& tl, const TeamArgs& ta
 
 // the team has arrived at `target`: lane 0 polls (sc1), the workgroup barrier releases the rest
 __device__ __forceinline__ void team_wait(const TeamArgs& ta, unsigned* ctr, unsigned target) {
-  if (threadIdx.x == 0) {
+  if (__builtin_amdgcn_workitem_id_x() == 0) {
     unsigned it = 0;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(8);
@@ -635,9 +635,9 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
                                                         float* __restrict__ y, int L, TeamArgs ta) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   using G = Geo<MODE, true>;
-  const int team = blockIdx.x / ta.TT, tile = blockIdx.x - team * ta.TT;
+  const int team = __builtin_amdgcn_workgroup_id_x() / ta.TT, tile = __builtin_amdgcn_workgroup_id_x() - team * ta.TT;
   const __amdgpu_buffer_rsrc_t hs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(ta.hsave + (size_t)blockIdx.x * WB * 64 * 4), 0, WB * 64 * 4, 0x00020000);
+      (void*)(ta.hsave + (size_t)__builtin_amdgcn_workgroup_id_x() * WB * 64 * 4), 0, WB * 64 * 4, 0x00020000);
   unsigned* ctr = ta.counters + (size_t)team * TEAM_CTR_STRIDE;
   char* tslots = ta.slots + (size_t)team * 2 * ta.TT * SLOT_BYTES;
   constexpr int NL = ADS ? 32 : 30;             // big layers
@@ -712,8 +712,8 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
     __syncthreads();                 // the next spectrum's stem overwrites the rows the head read
     stamp(6);
   }
-  if (RDN_TEAM_STAMPS && threadIdx.x == 0 && ta.stamps)
-    for (int k = 0; k < NSTAMP; ++k) ta.stamps[(size_t)blockIdx.x * NSTAMP + k] = stamp.acc[k];
+  if (RDN_TEAM_STAMPS && __builtin_amdgcn_workitem_id_x() == 0 && ta.stamps)
+    for (int k = 0; k < NSTAMP; ++k) ta.stamps[(size_t)__builtin_amdgcn_workgroup_id_x() * NSTAMP + k] = stamp.acc[k];
 }
 
 }  // namespace cb

@@ -56,6 +56,13 @@ typedef bf16x8 V;
 
 __device__ __forceinline__ f32x4 mma(V a, V b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
 
+// Thread index the compiler cannot treat as loop-invariant (per-lane addresses are recomputed where
+// they are used instead of being hoisted across the network's layers and spilled)
+__device__ __forceinline__ int tid() {
+  int t = __builtin_amdgcn_workitem_id_x();
+  asm volatile("" : "+v"(t));
+  return t;
+}
 __device__ __forceinline__ int soff(int row, int slot) { return row * ROWB + ((slot ^ (row & 7)) << 4); }
 __device__ __forceinline__ int wrap(int row) { return row < 0 ? row + WB : (row >= WB ? row - WB : row); }
 __device__ __forceinline__ bool in_range(int p, int L) { return (unsigned)p < (unsigned)L; }
@@ -83,14 +90,14 @@ struct Frags {            // one layer's operands in VGPRs: A-fragments and fold
 // the 28 loads of a layer cost no address VALU.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ V load_frag(const Tile& tl, int layer, int m, int s) {
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, (threadIdx.x & 63) * 16,
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, (tid() & 63) * 16,
                                                         layer * LAYER_BYTES + (m * 6 + s) * 1024, 0);
   return __builtin_bit_cast(V, v);
 }
 
 // lane quarter q's 4 output channels of M-tile m
 __device__ __forceinline__ f32x4 load_bias(const Tile& tl, int layer, int m) {
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, ((threadIdx.x & 63) >> 4) * 16,
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, ((tid() & 63) >> 4) * 16,
                                                         layer * LAYER_BYTES + BIAS_OFF + 64 * m, 0);
   return __builtin_bit_cast(f32x4, v);
 }
@@ -112,7 +119,7 @@ __device__ __forceinline__ void stem(const Tile& tl, int sslot, uint32_t dst) {
   const float* swp = tl.small + sslot * SMALL_SLOT_FLOATS;
   asm volatile("" : "+s"(swp));      // no reuse of scalar-loaded weights across the layers in between
   const cfloat* sw = (const cfloat*)swp;
-  for (int i = threadIdx.x; i < WB * 8; i += THREADS) {
+  for (int i = tid(); i < WB * 8; i += THREADS) {
     const int g = __builtin_amdgcn_readfirstlane(i / WB);
     const int row = i - g * WB;
     const int p = tl.base + row;
@@ -172,7 +179,7 @@ struct BAddr {
 template <int EPI, int NM, bool EDGE>
 __device__ __forceinline__ void conv(Tile& tl, uint32_t src, uint32_t dst, int dil, Frags& F, bool has_next,
                                      float (&out)[NT]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4, c16 = lane & 15;
+  const int lane = tid() & 63, w = tid() >> 6, q = lane >> 4, c16 = lane & 15;
   const int r0 = w * RW + c16;
   const int next = tl.layer + 1;
   const BAddr ba(src, r0, dil, q);
@@ -267,7 +274,7 @@ __device__ __forceinline__ void head(Tile& tl, uint32_t src, Frags& F, bool has_
 
 __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const float* x, int L, int T, int tiles,
                                           int halo, int& n_out) {
-  const int n = blockIdx.x / tiles, tile = blockIdx.x - n * tiles;
+  const int n = __builtin_amdgcn_workgroup_id_x() / tiles, tile = __builtin_amdgcn_workgroup_id_x() - n * tiles;
   n_out = n;
   Tile tl;
   tl.lds = lds;
@@ -283,10 +290,10 @@ __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const 
   return tl;
 }
 
-__device__ __forceinline__ int head_row(int k) { return (threadIdx.x >> 6) * RW + 16 * k + (threadIdx.x & 15); }
+__device__ __forceinline__ int head_row(int k) { return (tid() >> 6) * RW + 16 * k + (tid() & 15); }
 
 __device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, const float (&v)[NT], int halo, int T) {
-  if ((threadIdx.x & 63) >= 16) return;
+  if ((tid() & 63) >= 16) return;
 #pragma unroll
   for (int k = 0; k < NT; ++k) {
     const int j = head_row(k);
@@ -345,7 +352,7 @@ H16_BODY(rrcdnet) {
   float l[NT];
   head<EDGE>(tl, cur, F, false, l);
   // y = x - (right + left) / 2 on this tile's output rows (the lanes that stored r re-read it)
-  if ((threadIdx.x & 63) < 16) {
+  if ((tid() & 63) < 16) {
 #pragma unroll
     for (int k = 0; k < NT; ++k) {
       const int j = head_row(k);

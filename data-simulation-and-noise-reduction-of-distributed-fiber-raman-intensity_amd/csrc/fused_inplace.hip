@@ -56,7 +56,7 @@ IP_BODY(rrcdnet) {
   head<MODE, NBK>(tl, 3, l);
 #pragma unroll
   for (int k = 0; k < HEAD_ROWS; ++k) {
-    const int p = tl.base + (int)threadIdx.x + THREADS * k;
+    const int p = tl.base + (int)__builtin_amdgcn_workitem_id_x() + THREADS * k;
     const float xv = in_range(p, L) ? tl.x[p] : 0.f;
     r[k] = xv - (r[k] + l[k]) / 2.0f;
   }
@@ -119,7 +119,7 @@ IP_BODY(pidn) {
     extern __shared__ __attribute__((aligned(16))) char lds[];                                             \
     int n;                                                                                                 \
     Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(arch), n);                                   \
-    if (RDN_IP_PRIO && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);  \
+    if (RDN_IP_PRIO && __builtin_amdgcn_readfirstlane(__builtin_amdgcn_workitem_id_x()) >= 256) __builtin_amdgcn_s_setprio(1);  \
     if (tl.base >= 0 && tl.base + TileGeo<NetGeo<arch>::NBK>::WB <= L) name##_body<MODE, false>(tl, y, n, L, T); \
     else name##_body<MODE, true>(tl, y, n, L, T);                                                          \
   }

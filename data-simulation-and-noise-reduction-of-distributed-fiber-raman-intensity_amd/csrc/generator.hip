@@ -67,7 +67,7 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, fl
 template <typename T, typename Op>
 __device__ __forceinline__ T block_reduce(T v, T* scratch, Op op) {
   for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o));
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_workitem_id_x() >> 6, lane = __builtin_amdgcn_workitem_id_x() & 63;
   __syncthreads();
   if (lane == 0) scratch[w] = v;
   __syncthreads();
@@ -85,12 +85,12 @@ __global__ __launch_bounds__(GT) void generate_kernel(uint64_t seed, uint64_t fi
   __shared__ float s_spk[3][3];      // start, width, signed amplitude
   __shared__ int s_nspk;
   __shared__ float s_sigma;
-  const int tid = threadIdx.x;
-  const uint64_t idx = first + blockIdx.x;
+  const int tid = __builtin_amdgcn_workitem_id_x();
+  const uint64_t idx = first + __builtin_amdgcn_workgroup_id_x();
   const uint32_t ilo = (uint32_t)idx, ihi = (uint32_t)(idx >> 32);
   const int L = prm.L;
-  float* cl = clean + (size_t)blockIdx.x * L;
-  float* nz = noisy + (size_t)blockIdx.x * L;
+  float* cl = clean + (size_t)__builtin_amdgcn_workgroup_id_x() * L;
+  float* nz = noisy + (size_t)__builtin_amdgcn_workgroup_id_x() * L;
 
   // ---- phase A: piecewise-constant segments (raw values into `clean`) --------------------------
   float mn = INFINITY, mx = -INFINITY;
@@ -151,8 +151,8 @@ __global__ __launch_bounds__(GT) void generate_kernel(uint64_t seed, uint64_t fi
     }
     s_nspk = ns;
     s_sigma = sigma;
-    if (snr_out) snr_out[blockIdx.x] = snr;
-    if (std_out) std_out[blockIdx.x] = sigma;
+    if (snr_out) snr_out[__builtin_amdgcn_workgroup_id_x()] = snr;
+    if (std_out) std_out[__builtin_amdgcn_workgroup_id_x()] = sigma;
   }
   __syncthreads();
   const float sigma = s_sigma;

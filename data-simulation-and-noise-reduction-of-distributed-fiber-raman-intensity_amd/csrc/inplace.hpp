@@ -68,7 +68,7 @@ __device__ __forceinline__ bool in_range(int p, int L) { return p >= 0 && p < L;
 // recomputed where they are used instead of being hoisted out of the callers' layer / spectrum
 // loops (where, with 256 VGPRs taken by the conv, they are spilled to scratch and reloaded).
 __device__ __forceinline__ int opaque_tid() {
-  int t = threadIdx.x;
+  int t = __builtin_amdgcn_workitem_id_x();
   asm volatile("" : "+v"(t));
   return t;
 }
@@ -285,7 +285,7 @@ template <> struct Op<MODE_H8> {
     put(act, ad[0] + off, ad[1] + off, ad[2] + off, v);
   }
   __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc, uint32_t sa, int s) {
-    const int sb = (threadIdx.x & 32) ? H8_LO_E8M0 : H8_HI_E8M0;   // lanes 32-63: the lo blocks
+    const int sb = (__builtin_amdgcn_workitem_id_x() & 32) ? H8_LO_E8M0 : H8_HI_E8M0;   // lanes 32-63: the lo blocks
     if (s == 0) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 0, (int)sa, 0, sb);
     else if (s == 1) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 1, (int)sa, 0, sb);
     else acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 2, (int)sa, 0, sb);
@@ -303,7 +303,7 @@ template <> struct Op<MODE_H8> {
 };
 
 __device__ __forceinline__ void zero_guards(char* lds) {
-  const int t = threadIdx.x;           // 4 guard rows x 256 B = 64 lanes x 16 B
+  const int t = __builtin_amdgcn_workitem_id_x();           // 4 guard rows x 256 B = 64 lanes x 16 B
   if (t < 64) {
     const int r = t >> 4, slot = t & 15;
     const int prow = r < 2 ? r : ROWS - 4 + r;
@@ -349,7 +349,7 @@ __device__ __forceinline__ void stem(const Tile& tl, int slot) {
   }
 }
 
-// Conv1d(64, 1, 3, padding=1), one row per thread (row j = threadIdx.x + THREADS * k in out[k]),
+// Conv1d(64, 1, 3, padding=1), one row per thread (row j = __builtin_amdgcn_workitem_id_x() + THREADS * k in out[k]),
 // fp32 weights and accumulate.
 constexpr int HEAD_ROWS = 2;      // rows per thread: ceil(640 / 512)
 template <int MODE, int NBK = 4>
@@ -401,11 +401,11 @@ struct LayerA {
 
 template <int MODE>
 __device__ __forceinline__ f32x4 load_bias(const uint8_t* wl, int m) {
-  return *(const f32x4*)(wl + LayerBytes<MODE>::BIAS + (16 * m + 4 * ((threadIdx.x & 63) >> 4)) * 4);
+  return *(const f32x4*)(wl + LayerBytes<MODE>::BIAS + (16 * m + 4 * ((__builtin_amdgcn_workitem_id_x() & 63) >> 4)) * 4);
 }
 template <int MODE>
 __device__ __forceinline__ uint32_t load_scale(const uint8_t* wl, int m) {
-  return MODE == MODE_H8 ? ((const uint32_t*)(wl + H8_SCALE_OFF))[m * 64 + (threadIdx.x & 63)] : 0u;
+  return MODE == MODE_H8 ? ((const uint32_t*)(wl + H8_SCALE_OFF))[m * 64 + (__builtin_amdgcn_workitem_id_x() & 63)] : 0u;
 }
 
 template <int MODE>
@@ -505,11 +505,43 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #endif
     O::store4_at(tl.lds, sadr[mm], (uint32_t)(BR * j + 16 * i) * ROWB_F32, v);
   };
+  // MODE_H8: both M-tiles of N-tile i in one write-back, 16-B f16 slot + two 8-B e4m3 slots (3
+  // stores instead of 6); ReLU folded into the saturating med3
+  auto store_pair = [&](int j, int i) {
+    const int rb = BR * j + (BR / 4) * nq;
+    const bool inside = !EDGE || (tl.base + rb >= 0 && tl.base + rb + BR / 4 <= tl.L);
+    const bool zero = !inside && !in_range(tl.base + rb + 16 * i + c16, tl.L);
+    H8Split x[MT];
+#pragma unroll
+    for (int mm = 0; mm < MT; ++mm) {
+      f32x4 v = res[j][i][mm];
+      if (EPI & ADD_ID) v += id[(j * NT + i) * MT + mm];
+      v = (EPI & RELU) ? h8_sat<true>(v) : h8_sat<false>(v);
+      if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
+      x[mm] = h8_split(v);
+    }
+    const uint32_t off = (uint32_t)(BR * j + 16 * i) * ROWB_F32;
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+#if defined(RDN_ABLATE_NOSTORE)
+    if (x[0].hi8 == 0x12345678u)
+#endif
+    {
+      *(f16x8*)(tl.lds + sadr[0][0] + off) = __builtin_shufflevector(x[0].hi, x[1].hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      *(u32x2*)(tl.lds + sadr[0][1] + off) = u32x2{x[0].hi8, x[1].hi8};
+      *(u32x2*)(tl.lds + sadr[0][2] + off) = u32x2{x[0].lo8, x[1].lo8};
+    }
+  };
   auto store_block = [&](int j) {
+    if constexpr (MODE == MODE_H8) {
 #pragma unroll
-    for (int i = 0; i < NT; ++i)
+      for (int i = 0; i < NT; ++i) store_pair(j, i);
+    } else {
 #pragma unroll
-      for (int mm = 0; mm < MT; ++mm) store_piece(j, i, mm);
+      for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int mm = 0; mm < MT; ++mm) store_piece(j, i, mm);
+    }
   };
 
   // B fragments are software-pipelined one k-step ahead: the reads for k-step s+1 are issued
@@ -568,10 +600,12 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #if RDN_IP_SPREAD_STORE
       // lagged write-back of block j-2, one (N-tile, M-tile) piece per k-step: the LDS write
       // bursts of the 8 waves spread over the block instead of landing on its first k-step
-      // (NT * MT = 4 pieces over KSTEPS = 3 (MODE_H8), 6 or 12 k-steps)
+      // (MODE_H8: one N-tile's M-tile pair per k-step)
       if (j >= 2) {
         constexpr int NP = NT * MT;
-        if constexpr (O::KSTEPS >= NP) {
+        if constexpr (MODE == MODE_H8) {
+          if (s < NT) store_pair(j - 2, s);
+        } else if constexpr (O::KSTEPS >= NP) {
           if (s < NP) store_piece(j - 2, s / MT, s % MT);
         } else {
 #pragma unroll
@@ -597,7 +631,11 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #pragma unroll
       for (int i = 0; i < NT; ++i) bnext[i] = read_b(j + 1, 0, i);
     }
+#if defined(RDN_ABLATE_NOBARRIER)         // diagnostic builds only (tools/ablate.py): wrong results
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
     lds_barrier();                 // every wave is done reading the rows block j needed
+#endif
   }
   store_block(NB - 2);
   store_block(NB - 1);
@@ -613,7 +651,7 @@ template <> struct Geo<MODE_F32, false> { static constexpr int S = 2; };
 
 __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const float* x, int L, int T,
                                           int tiles, int halo, int& n_out) {
-  const int n = blockIdx.x / tiles, tile = blockIdx.x - n * tiles;
+  const int n = __builtin_amdgcn_workgroup_id_x() / tiles, tile = __builtin_amdgcn_workgroup_id_x() - n * tiles;
   n_out = n;
   Tile tl;
   tl.lds = lds;

@@ -17,7 +17,7 @@ constexpr int MT = 256;
 template <typename T, typename Op>
 __device__ __forceinline__ T block_reduce(T v, T* scratch, Op op) {
   for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o));
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_workitem_id_x() >> 6, lane = __builtin_amdgcn_workitem_id_x() & 63;
   __syncthreads();
   if (lane == 0) scratch[w] = v;
   __syncthreads();
@@ -29,9 +29,9 @@ __device__ __forceinline__ T block_reduce(T v, T* scratch, Op op) {
 __global__ __launch_bounds__(MT) void metrics_kernel(const float* __restrict__ y, const float* __restrict__ clean,
                                                      int L, double* __restrict__ per, double* __restrict__ sums) {
   __shared__ double red[MT / 64];
-  const int tid = threadIdx.x;
-  const float* yy = y + (size_t)blockIdx.x * L;
-  const float* cc = clean + (size_t)blockIdx.x * L;
+  const int tid = __builtin_amdgcn_workitem_id_x();
+  const float* yy = y + (size_t)__builtin_amdgcn_workgroup_id_x() * L;
+  const float* cc = clean + (size_t)__builtin_amdgcn_workgroup_id_x() * L;
   const auto add = [](double a, double b) { return a + b; };
   const auto mx = [](double a, double b) { return a > b ? a : b; };
   const auto mn = [](double a, double b) { return a < b ? a : b; };
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(MT) void metrics_kernel(const float* __restrict__ y
   if (tid == 0) {
     const double m4[4] = {se / L, ss / (L - 6), sm / (L - 1), ymax - ymin};
     if (per) {
-      for (int k = 0; k < 4; ++k) per[(size_t)blockIdx.x * 4 + k] = m4[k];
+      for (int k = 0; k < 4; ++k) per[(size_t)__builtin_amdgcn_workgroup_id_x() * 4 + k] = m4[k];
     }
     if (sums) {
       for (int k = 0; k < 4; ++k) atomicAdd(&sums[k], m4[k]);

@@ -20,14 +20,14 @@ VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "pf3": "-DRDN_H16_PF=3", "ieee": "", "nospread": "-DRDN_IP_SPREAD_STORE=0", "prio": "-DRDN_IP_PRIO=1",
             "prionospread": "-DRDN_IP_PRIO=1 -DRDN_IP_SPREAD_STORE=0", "stamps": "-DRDN_TEAM_STAMPS=1",
             "stamps_pre0": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_ID_PRE=0", "stamps_reload": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_RELOAD_A=1",
-            "stamps_pre16": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_ID_PRE=16", "h8generic": "-DRDN_H8_GENERIC=1"}
+            "stamps_pre16": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_ID_PRE=16", "nobar": "-DRDN_ABLATE_NOBARRIER"}
 
 
 def build():
     import torch
     tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
     os.makedirs(OUT, exist_ok=True)
-    srcs = ["fused16.hip", "fused_inplace.hip", "fused_h8.hip", "cbam.hip", "generator.hip", "metrics.hip", "abi.cpp",
+    srcs = ["fused16.hip", "fused_inplace.hip", "cbam.hip", "generator.hip", "metrics.hip", "abi.cpp",
             "pack.cpp"]
     only = sys.argv[2:]
     for name, flag in VARIANTS.items():
@@ -38,7 +38,7 @@ def build():
             o = os.path.join(OUT, f"{name}_{s}.o")
             cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mcode-object-version=5",
                    "-fno-gpu-rdc", "-c", os.path.join(CSRC, s), "-o", o] + flag.split()
-            if s in ("fused16.hip", "fused_inplace.hip", "fused_h8.hip", "cbam.hip") and name != "ieee":
+            if s in ("fused16.hip", "fused_inplace.hip", "cbam.hip") and name != "ieee":
                 cmd += ["-fno-honor-nans", "-mno-amdgpu-ieee"]
             if s == "generator.hip":
                 cmd += ["-ffp-contract=off"]
