@@ -120,7 +120,6 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
   const hipStream_t s = (hipStream_t)stream;
   const uint8_t* blob = (const uint8_t*)packed;
   if (is_cbam(arch)) {
-    if (dtype == RDN_F16F8) return fail(RDN_EUNSUPPORTED, "rdn_forward: RDN_F16F8 is not built for the CBAM networks");
     const size_t need = rdn::cbam_workspace_bytes(arch, dtype, n, L);
     if (ws_bytes < need || (need && !ws))
       return fail(RDN_ESIZE, "rdn_forward: workspace too small, need " + std::to_string(need) + " bytes");

@@ -372,7 +372,14 @@ __device__ __forceinline__ void save_identity(const Tile& tl, __amdgpu_buffer_rs
 template <int MODE>
 __device__ __forceinline__ void load8(const char* lds, int r, int k, float (&v)[8]) {
   const int pr = r + GUARD;
-  if (MODE == MODE_F32) {
+  if (MODE == MODE_H8) {          // f16 + e4m3 planes in h16_channel order: two 4-channel reads
+    const f32x4 a = Op<MODE>::load4(lds, pr, 8 * k), b = Op<MODE>::load4(lds, pr, 8 * k + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = a[i];
+      v[4 + i] = b[i];
+    }
+  } else if (MODE == MODE_F32) {
     const f32x4 a = *(const f32x4*)(lds + off_f32(pr, 32 * k)), b = *(const f32x4*)(lds + off_f32(pr, 32 * k + 16));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -773,9 +780,10 @@ static hipError_t launch_team(int arch, int mode, const TeamGeo& g, const uint8_
   team_kernel_t k;
   if (mode == ip::MODE_F32) k = ads ? team_forward<ip::MODE_F32, true> : team_forward<ip::MODE_F32, false>;
   else if (mode == ip::MODE_X3) k = ads ? team_forward<ip::MODE_X3, true> : team_forward<ip::MODE_X3, false>;
+  else if (mode == ip::MODE_H8) k = ads ? team_forward<ip::MODE_H8, true> : team_forward<ip::MODE_H8, false>;
   else k = ads ? team_forward<ip::MODE_B1, true> : team_forward<ip::MODE_B1, false>;
-  static bool attr_set[3][2] = {};
-  const int mi = mode == ip::MODE_F32 ? 0 : mode == ip::MODE_X3 ? 1 : 2;
+  static bool attr_set[4][2] = {};
+  const int mi = mode;                                 // MODE_* are 0..3
   if (!attr_set[mi][ads]) {
     const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SEG_LDS_BYTES);
     if (e != hipSuccess) return e;
@@ -808,11 +816,12 @@ typedef void (*seg_kernel_t)(const uint8_t*, const float*, float*, int, int, int
 hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                void* ws, size_t ws_bytes, hipStream_t stream) {
   using namespace cb;
-  const int mode = dtype == F32 ? ip::MODE_F32 : dtype == BF16X3 ? ip::MODE_X3 : ip::MODE_B1;
+  const int mode = dtype == F32 ? ip::MODE_F32 : dtype == BF16X3 ? ip::MODE_X3 : dtype == F16F8 ? ip::MODE_H8 : ip::MODE_B1;
   const seg_kernel_t k = mode == ip::MODE_F32 ? segment<ip::MODE_F32>
-                         : mode == ip::MODE_X3 ? segment<ip::MODE_X3> : segment<ip::MODE_B1>;
-  static bool attr_set[3] = {};
-  const int mi = mode == ip::MODE_F32 ? 0 : mode == ip::MODE_X3 ? 1 : 2;
+                         : mode == ip::MODE_X3 ? segment<ip::MODE_X3>
+                         : mode == ip::MODE_H8 ? segment<ip::MODE_H8> : segment<ip::MODE_B1>;
+  static bool attr_set[4] = {};
+  const int mi = mode;
   if (!attr_set[mi]) {
     const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SEG_LDS_BYTES);
     if (e != hipSuccess) return e;

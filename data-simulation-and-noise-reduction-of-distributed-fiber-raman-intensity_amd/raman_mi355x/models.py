@@ -48,7 +48,7 @@ class _EngineNet(nn.Module):
         """'fp32' (exact-fp32 MFMA, 1e-5 parity), 'bf16' (one bf16 MFMA per product, fastest) or
         'bf16x3' (split-bf16, three bf16 MFMAs per product: bf16 speed class, ~1e-4 accuracy) or
         'f16f8' (f16 product + one block-scaled e4m3 MFMA for both correction terms, ~1e-3 accuracy
-        at 2/3 of bf16x3's MFMA cycles; non-CBAM networks)."""
+        at 2/3 of bf16x3's MFMA cycles)."""
         code = engine._dtype(dtype)
         self._engine_dtype = {0: "fp32", 1: "bf16", 2: "bf16x3", 3: "f16f8"}[code]
         return self

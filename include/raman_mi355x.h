@@ -52,8 +52,7 @@ typedef enum {
  *   RDN_F16F8  f16 main product (v = hi + lo, hi = f16(v)) plus both correction products
  *              W_lo*X_hi + W_hi*X_lo as ONE block-scaled e4m3 MFMA at twice the 16-bit rate; f16 hi
  *              + e4m3 lo activations (~15 significant bits).  2e-2-safe at 2/3 of the MFMA cycles
- *              of RDN_BF16X3.  Non-CBAM networks only (CBAM networks: RDN_EUNSUPPORTED);
- *              activations must stay below the f16 range (65504). */
+ *              of RDN_BF16X3.  Activations saturate at +-1792 (the e4m3 range of hi / 4). */
 typedef enum { RDN_F32 = 0, RDN_BF16 = 1, RDN_BF16X3 = 2, RDN_F16F8 = 3 } rdn_dtype;
 
 enum {

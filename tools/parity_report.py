@@ -35,8 +35,6 @@ def main():
         for which in whichs:
             sd = golden_state_dict(arch, which)
             for dtype in ("fp32", "f16f8", "bf16x3", "bf16"):
-                if dtype == "f16f8" and arch in ("ADSDN", "APIDN"):
-                    continue                     # f16f8 is built for the non-CBAM networks
                 m = R.MODELS[arch]()
                 m.load_state_dict(sd)
                 m = m.cuda().eval().set_engine_dtype(dtype)

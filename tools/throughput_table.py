@@ -34,8 +34,6 @@ def main():
     for arch in args.archs:
         for L in ([10000, 16384] if arch in ("PIDN", "APIDN") else [10000]):
             for dt in args.dtypes:
-                if dt == "f16f8" and arch in ("ADSDN", "APIDN"):
-                    continue
                 B = {"bf16": 4096, "bf16x3": 2048, "f16f8": 2048, "fp32": 1024}[dt]
                 if arch in ("ADSDN", "APIDN"):
                     B //= 2
