@@ -19,3 +19,14 @@ for dt in f16f8 bf16x3 bf16; do
     rc=$?; echo "pmc $dt $tag rc=$rc"; if [ $rc -ne 0 ]; then tail -3 $OUT/pmc_${dt}_$tag.log; exit $rc; fi
   done
 done
+timeout -k 10 400 python -u tools/throughput_table.py --out $OUT/throughput.md > $OUT/throughput.log 2>&1
+rc=$?; echo "throughput rc=$rc"; if [ $rc -ne 0 ]; then tail -3 $OUT/throughput.log; exit $rc; fi
+mkdir -p gpurun_out/unf
+for dt in fp32 bf16; do
+  timeout -k 10 240 python -u tools/unfused_baseline.py --dtype $dt --out gpurun_out/unf/unfused_$dt.json > gpurun_out/unf/unfused_$dt.log 2>&1
+  rc=$?; echo "unfused $dt rc=$rc"; if [ $rc -ne 0 ]; then tail -3 gpurun_out/unf/unfused_$dt.log; exit $rc; fi
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 150 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/unf/pmc_${dt}_$ctr -o p -- python3 tools/unfused_baseline.py --dtype $dt --steps 2 --warmup 2 --batch 64 > gpurun_out/unf/pmc_${dt}_$ctr.log 2>&1
+    rc=$?; echo "pmc unfused $dt $ctr rc=$rc"; if [ $rc -ne 0 ]; then tail -3 gpurun_out/unf/pmc_${dt}_$ctr.log; exit $rc; fi
+  done
+done

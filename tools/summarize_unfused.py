@@ -15,12 +15,14 @@ import os
 import sys
 
 BATCH = 64
+MIN_K = 120
 
 
 def total_kib(d, counter):
-    """KiB of `counter` summed over the dispatches of ONE steady-state forward: the run ends with 2
-    identical forwards, so the forward is the shortest period K of the dispatch-name sequence with
-    names[-K:] == names[-2K:-K] (earlier dispatches include MIOpen's find-mode benchmarking)."""
+    """KiB of `counter` summed over the dispatches of ONE steady-state forward: the run's last
+    forwards are identical, so the forward is the shortest period K >= MIN_K of the dispatch-name
+    sequence ending at e (names[e-K:e] == names[e-2K:e-K]), e scanned back over the trailing
+    non-forward dispatches (earlier dispatches include MIOpen's find-mode benchmarking)."""
     per = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
@@ -31,9 +33,12 @@ def total_kib(d, counter):
                     per[i] = (name, v + float(r["Counter_Value"]))
     seq = [per[i] for i in sorted(per)]
     names = [n for n, _ in seq]
-    for k in range(1, len(seq) // 2 + 1):
-        if names[-k:] == names[-2 * k:-k]:
-            return sum(v for _, v in seq[-k:]), k
+    # the run ends with a few non-forward dispatches (isfinite check); a forward is > MIN_K
+    # dispatches, longer than the 7-dispatch-per-layer period inside one conv stack
+    for e in range(len(seq), len(seq) - 40, -1):
+        for k in range(MIN_K, e // 2 + 1):
+            if names[e - k:e] == names[e - 2 * k:e - k]:
+                return sum(v for _, v in seq[e - k:e]), k
     raise RuntimeError(f"{d}: no repeated forward at the end of the dispatch sequence")
 
 
