@@ -27,6 +27,9 @@ constexpr int MODE_F32 = 0, MODE_B1 = 1, MODE_X3 = 2, MODE_H8 = 3;
 #ifndef RDN_IP_SPREAD_STORE
 #define RDN_IP_SPREAD_STORE 1
 #endif
+#ifndef RDN_IP_NTPIPE
+#define RDN_IP_NTPIPE 1
+#endif
 constexpr uint32_t LDS_BYTES = ACT_BYTES_F32;                    // 132096 (512 rows + guards)
 
 // Tile geometry by number of 128-row blocks: NBK = 4 -> 512 rows with 2 zero guard rows per side
@@ -212,6 +215,9 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4v __attribute__((ext_vector_type(4)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
+#ifndef RDN_H8_FASTSPLIT
+#define RDN_H8_FASTSPLIT 1
+#endif
 // 4 floats -> 4 e4m3 bytes of v / div (v_cvt_scalef32_pk_fp8_f32: the division is free)
 __device__ __forceinline__ uint32_t pk_e4m3_div(f32x4 v, float div) {
   s16x2 o = {0, 0};
@@ -239,8 +245,23 @@ struct H8Split {
 };
 __device__ __forceinline__ H8Split h8_split(f32x4 r) {
   const f16x4 h = __builtin_convertvector(r, f16x4);
+#if RDN_H8_FASTSPLIT
+  // lo = r - f32(h) in one v_fma_mix_f32 per value (f16 source operand, exact), and the e4m3 copy
+  // of hi converted from r itself (its 3-bit mantissa cannot tell r from f16(r) except at
+  // double-rounding ties): no f16 -> f32 round trip.  14 VALU per 4 values instead of 18.
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 hb = __builtin_bit_cast(u32x2, h);
+  f32x4 lo;
+  // the compiler turns fma(f32(h), -1, r) into cvt + sub; the mixed-precision FMA is spelled out
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo[0]) : "v"(hb.x), "v"(r[0]));
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(lo[1]) : "v"(hb.x), "v"(r[1]));
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo[2]) : "v"(hb.y), "v"(r[2]));
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(lo[3]) : "v"(hb.y), "v"(r[3]));
+  return H8Split{h, pk_e4m3_div(r, H8_HI_DIV), pk_e4m3_div(lo, H8_LO_DIV)};
+#else
   const f32x4 g = __builtin_convertvector(h, f32x4);
   return H8Split{h, pk_e4m3_div(g, H8_HI_DIV), pk_e4m3_div(r - g, H8_LO_DIV)};
+#endif
 }
 
 template <> struct LayerBytes<MODE_H8> {
@@ -565,6 +586,38 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #pragma unroll
       for (int mm = 0; mm < MT; ++mm) a.bias[mm] = load_bias<MODE>(wnext, MT * mp + mm), a.sc[mm] = load_scale<MODE>(wnext, MT * mp + mm);
     }
+#if RDN_IP_NTPIPE
+    // B fragments rotate per N-tile: the reads of N-tile i for the next k-step (or for k-step 0 of
+    // block j+1) are issued as soon as its MFMAs of this k-step are issued, so they fly under the
+    // MFMAs of the other N-tile(s) instead of trailing the whole k-step -- same VGPRs as one set.
+#pragma unroll
+    for (int s = 0; s < O::KSTEPS; ++s) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+#pragma unroll
+        for (int mm = 0; mm < MT; ++mm) part[s % S][i][mm] = O::mma(a[mm][s], bnext[i], part[s % S][i][mm], sc_l[mm], s);
+        if (s + 1 < O::KSTEPS) bnext[i] = read_b(j, s + 1, i);
+        else if (j + 1 < NB) bnext[i] = read_b(j + 1, 0, i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (j == NB - 1 && has_next) {                                   // last use of a[.][s]
+#pragma unroll
+        for (int mm = 0; mm < MT; ++mm) a[mm][s] = O::load_a(wnext, MT * mp + mm, s, lane);
+      }
+      if (j >= 2) {
+        constexpr int NP = NT * MT;
+        if constexpr (MODE == MODE_H8) {
+          if (s < NT) store_pair(j - 2, s);
+        } else if constexpr (O::KSTEPS >= NP) {
+          if (s < NP) store_piece(j - 2, s / MT, s % MT);
+        } else {
+#pragma unroll
+          for (int pc = s * NP / O::KSTEPS; pc < (s + 1) * NP / O::KSTEPS; ++pc) store_piece(j - 2, pc / MT, pc % MT);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#else
 #pragma unroll
     for (int s = 0; s < O::KSTEPS; ++s) {
       typename O::B bcur[NT];
@@ -618,6 +671,11 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
       // keep B-fragment reads within their k-step (VGPR budget of 2 waves/SIMD)
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (j + 1 < NB) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) bnext[i] = read_b(j + 1, 0, i);
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll
@@ -627,10 +685,6 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
         for (int k = 1; k < S; ++k) v += part[k][i][mm];
         res[j][i][mm] = v;
       }
-    if (j + 1 < NB) {
-#pragma unroll
-      for (int i = 0; i < NT; ++i) bnext[i] = read_b(j + 1, 0, i);
-    }
 #if defined(RDN_ABLATE_NOBARRIER)         // diagnostic builds only (tools/ablate.py): wrong results
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #else
