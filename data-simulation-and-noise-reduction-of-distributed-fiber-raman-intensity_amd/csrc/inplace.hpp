@@ -30,6 +30,9 @@ constexpr int MODE_F32 = 0, MODE_B1 = 1, MODE_X3 = 2, MODE_H8 = 3;
 #ifndef RDN_IP_NTPIPE
 #define RDN_IP_NTPIPE 1
 #endif
+#ifndef RDN_IP_HIBASE
+#define RDN_IP_HIBASE 1
+#endif
 constexpr uint32_t LDS_BYTES = ACT_BYTES_F32;                    // 132096 (512 rows + guards)
 
 // Tile geometry by number of 128-row blocks: NBK = 4 -> 512 rows with 2 zero guard rows per side
@@ -495,9 +498,24 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
         blast[s][p] = pl * ROWB_F32 + ((O::bslot(2 * TS + s, q, p) ^ swz256(pl)) << 4);
       }
   }
+#if RDN_IP_HIBASE
+  // a second set of B addresses 64 KiB up: blocks 2 and 3 then fit the 16-bit ds_read offset
+  // (no v_add per read); block 4 still adds
+  uint32_t badr2[O::KSTEPS][O::PLANES];
+#pragma unroll
+  for (int s = 0; s < O::KSTEPS; ++s)
+#pragma unroll
+    for (int p = 0; p < O::PLANES; ++p) {
+      badr2[s][p] = badr[s][p] + 2 * BR * ROWB_F32;
+      asm volatile("" : "+v"(badr2[s][p]));         // a register of its own, not re-derived per read
+    }
+#endif
   auto read_b = [&](int j, int s, int i) -> typename O::B {
     if (TG::WRAP && j == 0 && s < TS && i == 0) return O::load_b_at(tl.lds, bfirst[s], 0);
     if (TG::WRAP && j == NB - 1 && s >= 2 * TS && i == NT - 1) return O::load_b_at(tl.lds, blast[s - 2 * TS], 0);
+#if RDN_IP_HIBASE
+    if (j >= 2) return O::load_b_at(tl.lds, badr2[s], (uint32_t)(BR * (j - 2) + 16 * i) * ROWB_F32);
+#endif
     return O::load_b_at(tl.lds, badr[s], (uint32_t)(BR * j + 16 * i) * ROWB_F32);
   };
 #pragma unroll
