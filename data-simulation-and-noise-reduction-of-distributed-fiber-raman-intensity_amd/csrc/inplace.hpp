@@ -223,7 +223,13 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 #endif
 // 4 floats -> 4 e4m3 bytes of v / div (v_cvt_scalef32_pk_fp8_f32: the division is free)
 __device__ __forceinline__ uint32_t pk_e4m3_div(f32x4 v, float div) {
+#if RDN_H8_FASTSPLIT
+  // both halves are overwritten: seed the tied destination with a source that dies here (v[0]),
+  // so no zero-initialising v_mov is needed
+  s16x2 o = __builtin_bit_cast(s16x2, v[0]);
+#else
   s16x2 o = {0, 0};
+#endif
   o = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(o, v[0], v[1], div, false);
   o = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(o, v[2], v[3], div, true);
   return __builtin_bit_cast(uint32_t, o);
