@@ -270,8 +270,9 @@ __global__ __launch_bounds__(THREADS) void segment(const uint8_t* __restrict__ b
 // The whole network in ONE launch.  The grid is `teams` x TT co-resident workgroups (one per CU:
 // the tile takes 143 KB of LDS); the TT workgroups of a team own the TT tiles of one spectrum and
 // walk the spectra team, team + teams, ...  Each keeps its tile (512 rows + the whole network's
-// halo, so no halo exchange is needed) in LDS from the stem to the head.  CBAM is pointwise except
-// the +-3-row spatial conv (inside the halo) and the channel pool over the whole spectrum: at each
+// TEAM_HALO rows per side, refreshed from the neighbours' published edge rows at every CBAM) in LDS
+// from the stem to the head.  CBAM is pointwise except the +-3-row spatial conv and the channel pool
+// over the whole spectrum: at each
 // CBAM every tile publishes the per-channel sum (fp64) and max of u over its own positions to a
 // slot, the team meets at a counter, and every tile reduces the TT slots in tile order (so the
 // result is deterministic) into ca.  Hand-off per MI355X_MICROARCH.md §Workgroup dispatch (first
@@ -281,7 +282,19 @@ __global__ __launch_bounds__(THREADS) void segment(const uint8_t* __restrict__ b
 // per-workgroup fp32 buffer in memory (sc1 stores / loads: written and read back by the same CU).
 // A wait that exceeds SPIN_LIMIT polls raises the error word and falls through instead of hanging.
 
-constexpr int SLOT_BYTES = 64 * 8 + 64 * 4;        // per-tile stats: 64 fp64 sums, 64 ordered u32 maxima
+// Halo exchange: the tiles of a team meet at every CBAM anyway, so instead of recomputing the whole
+// network's halo (85 / 77 rows per side for ADSDN / APIDN: 30 / 28 tiles per spectrum at L = 10,000)
+// each tile keeps TEAM_HALO rows per side and, with its statistics, publishes the EDGE_ROWS rows of
+// u its neighbours' halos need.  Between two CBAMs a tile runs at most 2 convs (k = 3, d = 1), so
+// with h valid on rows [3, WB - 3) after a CBAM, u is valid on [5, WB - 5) at the next one; the
+// neighbours supply rows [0, 5) and [WB - 5, WB), the +-3-row spatial conv then yields h valid on
+// [3, WB - 3) again, and the head (+-1 row) reads only rows inside it: TEAM_HALO >= 4.
+constexpr int TEAM_HALO = 6;
+constexpr int EDGE_ROWS = 5;
+constexpr int EDGE_BYTES = EDGE_ROWS * 64 * 4;       // one edge, fp32
+constexpr int STAT_BYTES = 64 * 8 + 64 * 4;        // per-tile stats: 64 fp64 sums, 64 ordered u32 maxima
+constexpr int SLOT_BYTES = STAT_BYTES + 2 * EDGE_BYTES;   // + the tile's first / last EDGE_ROWS own-edge rows
+static_assert(2 * TEAM_HALO - EDGE_ROWS >= TEAM_HALO - 1 && TEAM_HALO >= 4, "edge rows lie in the tile's own rows");
 constexpr unsigned SPIN_LIMIT = 1u << 22;          // ~0.3 s of s_sleep polls
 constexpr int TEAM_CTR_STRIDE = 16;                // u32s between team counters (64 B)
 
@@ -431,6 +444,17 @@ __device__ __forceinline__ void publish_stats(const Tile& tl, const TeamArgs& ta
       rm[w * 64 + 4 * sub + i] = f2ord(mx[i]);
     }
   }
+  // edge rows for the neighbours (sc1 stores, drained before the barrier that precedes the
+  // arrival): block 0 = rows [2H - 5, 2H) (the left neighbour's rows [WB - 5, WB)), block 1 = rows
+  // [T, T + 5) (the right neighbour's rows [0, 5))
+  if (tid < 2 * EDGE_ROWS * 16) {
+    const int e = tid / (EDGE_ROWS * 16), k = (tid / 16) % EDGE_ROWS, c4 = tid & 15;
+    const int r = e == 0 ? 2 * H - EDGE_ROWS + k : T + k;
+    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slot, 0, SLOT_BYTES, 0x00020000);
+    const f32x4 u = Op<MODE>::load4(lds, r + GUARD, 4 * c4);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, u), sr, STAT_BYTES + e * EDGE_BYTES + (k * 64 + 4 * c4) * 4, 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   st(8);
   __syncthreads();
   st(9);
@@ -546,6 +570,20 @@ __device__ __forceinline__ void apply_cbam(const Tile& tl, const TeamArgs& ta, c
       }
       red[tid] = (double)(float)(sum / (double)tl.L);
       red[64 + tid] = (double)ord2f(m);
+    }
+  }
+  // halo refresh: u of rows [0, 5) from the left neighbour's block 1, rows [WB - 5, WB) from the
+  // right neighbour's block 0 (first / last tile of a spectrum: no neighbour, rows outside [0, L))
+  if (tid < 2 * EDGE_ROWS * 16) {
+    const int tile = (tl.base + ta.halo) / ta.T;
+    const int e = tid / (EDGE_ROWS * 16), k = (tid / 16) % EDGE_ROWS, c4 = tid & 15;
+    const int nb = e == 0 ? tile - 1 : tile + 1;
+    if (nb >= 0 && nb < ta.TT) {
+      const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slots0, 0, ta.TT * SLOT_BYTES, 0x00020000);
+      const f32x4 u = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(sr, nb * SLOT_BYTES + STAT_BYTES + (1 - e) * EDGE_BYTES + (k * 64 + 4 * c4) * 4, 0, 16));
+      const int r = e == 0 ? k : WB - EDGE_ROWS + k;
+      Op<MODE>::store4(lds, r + GUARD, 4 * c4, u);
     }
   }
   __syncthreads();
@@ -731,8 +769,8 @@ static constexpr int64_t CBAM_CHUNK = 1024;       // spectra per pass (bounds th
 
 static size_t act_bytes(int64_t n, int64_t L) { return (size_t)n * L * 64 * sizeof(float); }
 
-// Team-persistent geometry: halo of the whole network (stem 1, conv 1 each, CBAM spatial conv 3,
-// head 1), TT tiles per spectrum, as many teams as fit one workgroup per CU.
+// Team-persistent geometry: TEAM_HALO rows per side (refreshed from the neighbours at every CBAM),
+// TT tiles per spectrum, as many teams as fit one workgroup per CU.
 struct TeamGeo {
   int halo, T, TT, teams;
   size_t slots, counters, hsave, total;
@@ -748,7 +786,7 @@ static int device_cus() {
 }
 static TeamGeo team_geo(int arch, int64_t L) {
   TeamGeo g{};
-  g.halo = arch == ADSDN ? 1 + 3 + 2 + 3 + 15 * 5 + 1 : 1 + 15 * 5 + 1;
+  g.halo = cb::TEAM_HALO;                  // halos refreshed from the neighbours at every CBAM
   g.T = WB - 2 * g.halo;
   g.TT = (int)((L + g.T - 1) / g.T);
   const int cus = device_cus();
