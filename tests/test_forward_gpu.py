@@ -170,3 +170,37 @@ def test_rejects_unsupported_use():
         m.eval()(x.cpu())                 # CPU tensor
     with pytest.raises(ValueError):
         m.eval()(torch.zeros(1, 2, 100, device="cuda"))
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "f16f8", "bf16x3"])
+@pytest.mark.parametrize("arch", ["ADSDN", "APIDN"])
+@pytest.mark.parametrize("L", [499, 500, 501, 1003, 1505, 4999])
+def test_cbam_team_halo_exchange(arch, L, dtype):
+    """CBAM team kernel tiles own T = 512 - 2*6 = 500 positions and refresh their 6-row halos from the
+    neighbours' published edge rows at every CBAM: tile-boundary lengths, incl. a last tile that owns
+    fewer positions (1003 = 2*500 + 3) than the 5 edge rows its neighbour reads, against the oracle."""
+    from oracle.models import forward as oracle_forward
+    sd = golden_state_dict(arch, "synth")
+    m = _model(arch, "synth", dtype)
+    rng = np.random.default_rng(L + 7)
+    x = rng.uniform(-0.2, 1.2, (2, L)).astype(np.float32)
+    y = _run(m, x)
+    ref = oracle_forward(arch, sd, torch.from_numpy(x).unsqueeze(1)).squeeze(1).numpy()
+    scale = max(np.abs(ref).max(), 1e-30)
+    err = np.abs(y - ref).max()
+    tol = F32_REL * scale if dtype == "fp32" else BF16_ABS * max(1.0, scale)
+    assert err <= tol, f"{arch} L={L} {dtype}: {err:.3e} > {tol:.3e}"
+
+
+@pytest.mark.parametrize("arch", ["ADSDN", "APIDN"])
+def test_cbam_team_matches_segment_path(arch, monkeypatch):
+    """The team-persistent kernel (halo exchange) and the per-segment launches (RDN_CBAM_SEGMENTS=1,
+    the fallback for spectra longer than the team geometry) agree to fp32 rounding."""
+    m = _model(arch, "synth", "fp32")
+    x = np.random.default_rng(3).uniform(0, 1, (3, 2600)).astype(np.float32)
+    y_team = _run(m, x)
+    monkeypatch.setenv("RDN_CBAM_SEGMENTS", "1")
+    y_seg = _run(m, x)
+    monkeypatch.delenv("RDN_CBAM_SEGMENTS")
+    scale = max(np.abs(y_seg).max(), 1e-30)
+    assert np.abs(y_team - y_seg).max() <= 2e-6 * scale, np.abs(y_team - y_seg).max() / scale
