@@ -358,15 +358,39 @@ __device__ __forceinline__ int pw_row(int w, int rgrp, int k) {
 // The ResidualBlock identity (the block input, all WB tile rows).  Plain bf16 keeps it in the free
 // lo plane of its own LDS row (the activation is bf16 there, so the copy is exact); fp32 and
 // split-bf16 park it as fp32 in the workgroup's buffer in memory.
+// f16f8 parks it in its own two-plane form (f16 hi + e4m3 lo: 12 B per 4 values instead of 16, the
+// value its LDS row holds): 96 KB per tile, so the 30 tiles of an XCD keep it in their 4 MB L2.
+// IdRaw: the identity as fetched (converted to f32 only where it is added).
+typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+template <int MODE> struct IdRaw { typedef u32x4 T; };
+template <> struct IdRaw<MODE_H8> { typedef u32x3 T; };
 template <int MODE>
 __device__ __forceinline__ void id_store(char* lds, __amdgpu_buffer_rsrc_t hs, int r, int sub, f32x4 h) {
   if (MODE == MODE_B1) *(bf16x4*)(lds + off_f32(r + GUARD, 128 + 8 * sub)) = __builtin_convertvector(h, bf16x4);
-  else hs_store(hs, (r * 64 + 4 * sub) * 4, h);
+  else if (MODE == MODE_H8) {
+    const H8Split x = h8_split(h8_sat<false>(h));
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 hb = __builtin_bit_cast(u32x2, x.hi);
+    __builtin_amdgcn_raw_buffer_store_b96(u32x3{hb.x, hb.y, x.lo8}, hs, (r * 16 + sub) * 12, 0, 16);
+  } else hs_store(hs, (r * 64 + 4 * sub) * 4, h);
+}
+template <int MODE>
+__device__ __forceinline__ typename IdRaw<MODE>::T id_fetch(__amdgpu_buffer_rsrc_t hs, int r, int sub) {
+  if constexpr (MODE == MODE_H8) return __builtin_amdgcn_raw_buffer_load_b96(hs, (r * 16 + sub) * 12, 0, 16);
+  else return __builtin_amdgcn_raw_buffer_load_b128(hs, (r * 64 + 4 * sub) * 4, 0, 16);
+}
+template <int MODE>
+__device__ __forceinline__ f32x4 id_value(typename IdRaw<MODE>::T v) {
+  if constexpr (MODE == MODE_H8) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const f16x4 hi = __builtin_bit_cast(f16x4, u32x2{v.x, v.y});
+    return __builtin_convertvector(hi, f32x4) + unpk_e4m3(v.z) * H8_LO_DIV;
+  } else return __builtin_bit_cast(f32x4, v);
 }
 template <int MODE>
 __device__ __forceinline__ f32x4 id_load(const char* lds, __amdgpu_buffer_rsrc_t hs, int r, int sub) {
   if (MODE == MODE_B1) return __builtin_convertvector(*(const bf16x4*)(lds + off_f32(r + GUARD, 128 + 8 * sub)), f32x4);
-  return hs_load(hs, (r * 64 + 4 * sub) * 4);
+  return id_value<MODE>(id_fetch<MODE>(hs, r, sub));
 }
 
 // block input (all WB tile rows) -> identity (used after the stem; later blocks save it from the
@@ -497,13 +521,13 @@ constexpr int ID_ITERS = WB / (WAVES * 4);          // rows per thread in the po
 #ifndef RDN_CBAM_RELOAD_A
 #define RDN_CBAM_RELOAD_A 0
 #endif
-// identity rows fetched ahead of the spatial pass (the rest at the write-back): all 16 for fp32,
-// 8 for split-bf16 (16 spill there; measured 18.8k vs 16.5k APIDN spectra/s); plain bf16 keeps
-// its identity in LDS
+// identity rows fetched ahead of the spatial pass (the rest at the write-back): all 16 for fp32 and
+// f16f8 (3 VGPRs per row there), 8 for split-bf16 (16 spill there; measured 18.8k vs 16.5k APIDN
+// spectra/s); plain bf16 keeps its identity in LDS
 #ifdef RDN_CBAM_ID_PRE
 template <int MODE> constexpr int ID_PRE = RDN_CBAM_ID_PRE;
 #else
-template <int MODE> constexpr int ID_PRE = MODE == MODE_F32 ? 16 : 8;
+template <int MODE> constexpr int ID_PRE = MODE == MODE_X3 ? 8 : 16;
 #endif
 
 template <int MODE>
@@ -611,10 +635,10 @@ __device__ __forceinline__ void apply_cbam(const Tile& tl, const TeamArgs& ta, c
 
   // -- identities of this thread's pointwise rows, in flight during the spatial pass
   const int sub = lane & 15, rgrp = lane >> 4;
-  f32x4 idr[ID_ITERS];
+  typename IdRaw<MODE>::T idr[ID_ITERS];
   if (MODE != MODE_B1 && res != RES_NONE) {
 #pragma unroll
-    for (int k = 0; k < ID_PRE<MODE>; ++k) idr[k] = hs_load(hs, (pw_row<MODE>(w, rgrp, k) * 64 + 4 * sub) * 4);
+    for (int k = 0; k < ID_PRE<MODE>; ++k) idr[k] = id_fetch<MODE>(hs, pw_row<MODE>(w, rgrp, k), sub);
   }
   // -- spatial statistics of u*ca: one tile row per thread (rows beyond the tile: 0; they feed
   //    only halo rows)
@@ -664,7 +688,7 @@ __device__ __forceinline__ void apply_cbam(const Tile& tl, const TeamArgs& ta, c
 #pragma unroll
     for (int i = 0; i < 4; ++i) h[i] = (u[i] * cav[i]) * sr;
     if (res != RES_NONE) {
-      h += MODE == MODE_B1 || k >= ID_PRE<MODE> ? id_load<MODE>(lds, hs, r, sub) : idr[k];
+      h += MODE == MODE_B1 || k >= ID_PRE<MODE> ? id_load<MODE>(lds, hs, r, sub) : id_value<MODE>(idr[k]);
       if (res == RES_ADD_RELU) h = __builtin_elementwise_max(h, f32x4{0.f, 0.f, 0.f, 0.f});
     }
     const int p = tl.base + r;
