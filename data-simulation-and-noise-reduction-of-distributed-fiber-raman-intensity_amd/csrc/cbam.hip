@@ -442,6 +442,16 @@ __device__ __forceinline__ void publish_stats(const Tile& tl, const TeamArgs& ta
   const int tid = opaque_tid(), lane = tid & 63, w = tid >> 6, sub = lane & 15, rgrp = lane >> 4;
   const int H = ta.halo, T = ta.T;
   const int rend = H + min(T, tl.L - tl.base - H);     // the last tile of a spectrum ends at L
+  // edge rows for the neighbours (sc1 stores, issued first so that they drain under the statistics
+  // pass): block 0 = rows [2H - 5, 2H) (the left neighbour's rows [WB - 5, WB)), block 1 = rows
+  // [T, T + 5) (the right neighbour's rows [0, 5))
+  if (tid < 2 * EDGE_ROWS * 16) {
+    const int e = tid / (EDGE_ROWS * 16), k = (tid / 16) % EDGE_ROWS, c4 = tid & 15;
+    const int r = e == 0 ? 2 * H - EDGE_ROWS + k : T + k;
+    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slot, 0, SLOT_BYTES, 0x00020000);
+    const f32x4 u = Op<MODE>::load4(lds, r + GUARD, 4 * c4);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, u), sr, STAT_BYTES + e * EDGE_BYTES + (k * 64 + 4 * c4) * 4, 0, 16);
+  }
   // fp32 partials over <= T / 32 rows per lane, fp64 from the cross-wave sum on
   f32x4 sm = {0.f, 0.f, 0.f, 0.f}, mx = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll 4
@@ -468,17 +478,9 @@ __device__ __forceinline__ void publish_stats(const Tile& tl, const TeamArgs& ta
       rm[w * 64 + 4 * sub + i] = f2ord(mx[i]);
     }
   }
-  // edge rows for the neighbours (sc1 stores, drained before the barrier that precedes the
-  // arrival): block 0 = rows [2H - 5, 2H) (the left neighbour's rows [WB - 5, WB)), block 1 = rows
-  // [T, T + 5) (the right neighbour's rows [0, 5))
-  if (tid < 2 * EDGE_ROWS * 16) {
-    const int e = tid / (EDGE_ROWS * 16), k = (tid / 16) % EDGE_ROWS, c4 = tid & 15;
-    const int r = e == 0 ? 2 * H - EDGE_ROWS + k : T + k;
-    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slot, 0, SLOT_BYTES, 0x00020000);
-    const f32x4 u = Op<MODE>::load4(lds, r + GUARD, 4 * c4);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, u), sr, STAT_BYTES + e * EDGE_BYTES + (k * 64 + 4 * c4) * 4, 0, 16);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  // the edge stores drain under the statistics pass; every storing wave waits for them before the
+  // barrier that precedes the arrival
+  if (tid < 2 * EDGE_ROWS * 16) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   st(8);
   __syncthreads();
   st(9);
@@ -550,6 +552,22 @@ __device__ __forceinline__ void apply_cbam(const Tile& tl, const TeamArgs& ta, c
   const f32x4 cw2v = *(const f32x4*)(cw2 + 4 * lane);              // channel lane's 4 hidden weights
   const float b2 = bias ? cmisc[4 + lane] : 0.f;
 
+  // -- halo refresh, fetched first so that its round trip overlaps the slots': u of rows [0, 5)
+  //    from the left neighbour's block 1, rows [WB - 5, WB) from the right neighbour's block 0
+  //    (first / last tile of a spectrum: no neighbour, rows outside [0, L))
+  const int edge_e = tid / (EDGE_ROWS * 16), edge_k = (tid / 16) % EDGE_ROWS;
+  bool has_edge = false;
+  f32x4 edge_u = {0.f, 0.f, 0.f, 0.f};
+  if (tid < 2 * EDGE_ROWS * 16) {
+    const int tile = (tl.base + ta.halo) / ta.T;
+    const int nb = edge_e == 0 ? tile - 1 : tile + 1;
+    if (nb >= 0 && nb < ta.TT) {
+      const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slots0, 0, ta.TT * SLOT_BYTES, 0x00020000);
+      edge_u = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+          sr, nb * SLOT_BYTES + STAT_BYTES + (1 - edge_e) * EDGE_BYTES + (edge_k * 64 + 4 * (tid & 15)) * 4, 0, 16));
+      has_edge = true;
+    }
+  }
   // -- the spectrum's per-channel mean and max over the TT slots: 8 tile-strided partials per
   //    channel (all waves, sc1 buffer loads issued together: they are L2 / fabric round trips),
   //    then combined in a fixed order (deterministic)
@@ -596,20 +614,8 @@ __device__ __forceinline__ void apply_cbam(const Tile& tl, const TeamArgs& ta, c
       red[64 + tid] = (double)ord2f(m);
     }
   }
-  // halo refresh: u of rows [0, 5) from the left neighbour's block 1, rows [WB - 5, WB) from the
-  // right neighbour's block 0 (first / last tile of a spectrum: no neighbour, rows outside [0, L))
-  if (tid < 2 * EDGE_ROWS * 16) {
-    const int tile = (tl.base + ta.halo) / ta.T;
-    const int e = tid / (EDGE_ROWS * 16), k = (tid / 16) % EDGE_ROWS, c4 = tid & 15;
-    const int nb = e == 0 ? tile - 1 : tile + 1;
-    if (nb >= 0 && nb < ta.TT) {
-      const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slots0, 0, ta.TT * SLOT_BYTES, 0x00020000);
-      const f32x4 u = __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(sr, nb * SLOT_BYTES + STAT_BYTES + (1 - e) * EDGE_BYTES + (k * 64 + 4 * c4) * 4, 0, 16));
-      const int r = e == 0 ? k : WB - EDGE_ROWS + k;
-      Op<MODE>::store4(lds, r + GUARD, 4 * c4, u);
-    }
-  }
+  // halo refresh (the edge rows fetched above): into rows [0, 5) / [WB - 5, WB)
+  if (has_edge) Op<MODE>::store4(lds, (edge_e == 0 ? edge_k : WB - EDGE_ROWS + edge_k) + GUARD, 4 * (tid & 15), edge_u);
   __syncthreads();
   st(10);
   // -- channel attention: hidden unit (w & 3) of the shared MLP for the avg (w < 4) or max pooled
