@@ -93,6 +93,47 @@ def time_forward(engine, arch, dtype, packed, x, y, steps, warmup, stream):
     return e0.elapsed_time(e1) / steps
 
 
+def time_pipeline(engine, arch, dtype, packed, seed, first, B, L, steps, stream, dev):
+    """SURVEY.md §8d configs 3-4 end to end, reported beside `value` (never as it): per step the
+    device simulator writes B fresh spectra (new indices each step), the fused forward denoises them
+    and the fp64 metric kernel accumulates the evaluate sums (evaulate.py:29-39) — no host sync,
+    nothing leaves HBM.  Also times each stage alone on the same buffers."""
+    clean = torch.empty((B, L), dtype=torch.float32, device=dev)
+    noisy = torch.empty((B, L), dtype=torch.float32, device=dev)
+    y = torch.empty((B, 1, L), dtype=torch.float32, device=dev)
+    sums = torch.zeros(5, dtype=torch.float64, device=dev)
+
+    def gen(i):
+        engine.generate(B, seed, first_index=first + i * B, signal_length=L, device=dev, out=(clean, noisy))
+
+    def fwd():
+        engine.forward(arch, dtype, packed, noisy.view(B, 1, L), out=y)
+
+    def met():
+        engine.metrics(y.view(B, L), clean, sums=sums, per_spectrum=False)
+
+    def timed(fn):
+        fn(0)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(steps):
+            fn(i + 1)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / steps
+
+    ms_gen = timed(gen)
+    ms_fwd = timed(lambda i: fwd())
+    ms_met = timed(lambda i: met())
+    sums.zero_()
+    ms_all = timed(lambda i: (gen(i), fwd(), met()))
+    return {"spectra_per_s_per_gpu": B / (ms_all * 1e-3), "ms_per_step": ms_all, "batch": B, "steps": steps,
+            "stage_ms": {"simulate": ms_gen, "forward": ms_fwd, "metrics": ms_met},
+            "spectra_metered": int(sums[4].item()),
+            "note": "simulate -> fused forward -> fp64 metric sums per step, all on device (configs 3-4)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -106,6 +147,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true", help="skip timing the other engine dtypes")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="skip timing the simulate -> forward -> metrics pipeline (SURVEY.md §8d configs 3-4)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -173,6 +216,11 @@ def main():
                             "roofline_frac": flops_per_spectrum(args.arch, L) * nb / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[dt]}
         model.set_engine_dtype(args.dtype)
 
+    pipeline = None
+    if not args.no_pipeline:
+        pipeline = time_pipeline(engine, args.arch, args.dtype, packed, args.seed, (world + rank) * B, B, L,
+                                 3, stream, dev)
+
     if rank == 0:
         total = world * B * args.steps
         fl = flops_per_spectrum(args.arch, L) * B              # per launch
@@ -195,6 +243,7 @@ def main():
                          "mfma_cost_per_product_bf16_units": MFMA_COST.get(args.dtype),
                          "executed_bf16_equiv_tflops": achieved * MFMA_COST[args.dtype] if args.dtype in MFMA_COST else None},
             "variants": variants,
+            "pipeline": pipeline,
             "metrics_mean": {k: sums[i] / sums[4] for i, k in enumerate(["MSE", "SSIM", "Smoothness", "Peak2Peak"])},
         }
         if world == 1 and not args.no_cpu_baseline:
