@@ -11,7 +11,7 @@ timeout -k 10 300 python -u tools/parity_report.py --out $OUT/parity.md > $OUT/p
 rc=$?; echo "parity rc=$rc"; if [ $rc -ne 0 ]; then tail -5 $OUT/parity.log; exit $rc; fi
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py > $OUT/kt_bench.log 2>&1
 rc=$?; echo "kt rc=$rc"; tail -1 $OUT/kt_bench.log | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi
-SHORT="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-variants"
+SHORT="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-variants --no-pipeline"
 for dt in f16f8 bf16x3 bf16; do
   for ctr in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
     tag=$(echo $ctr | cut -d' ' -f1)

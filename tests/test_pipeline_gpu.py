@@ -1,0 +1,75 @@
+"""The on-device evaluation pipeline bench.py times beside the headline:
+simulate -> fused forward -> fp64 metric sums, chunk by chunk into reused buffers, no host sync.
+
+Checks that chunking is invisible: the chunked run's spectra, outputs and accumulated metric sums
+equal one whole-batch run (simulator keyed on the global spectrum index, forward independent of
+batch neighbours), and that the pipeline's outputs and metrics match the CPU oracle on the same
+simulated inputs (oracle forward fp32 1e-5 relative / f16f8 2e-2 abs; metrics oracle 1e-10).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_state_dict
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20250410
+
+
+def _pipeline(model, arch, dtype, n, chunk, L, first=0):
+    from raman_mi355x import engine
+    dev = torch.device("cuda")
+    packed = model.packed_weights(dev)
+    clean = torch.empty((chunk, L), dtype=torch.float32, device=dev)
+    noisy = torch.empty((chunk, L), dtype=torch.float32, device=dev)
+    y = torch.empty((chunk, 1, L), dtype=torch.float32, device=dev)
+    sums = torch.zeros(5, dtype=torch.float64, device=dev)
+    xs, ys = [], []
+    for i0 in range(0, n, chunk):
+        engine.generate(chunk, SEED, first_index=first + i0, signal_length=L, device=dev, out=(clean, noisy))
+        engine.forward(arch, dtype, packed, noisy.view(chunk, 1, L), out=y)
+        engine.metrics(y.view(chunk, L), clean, sums=sums, per_spectrum=False)
+        xs.append(noisy.cpu().numpy().copy())
+        ys.append(y.view(chunk, L).cpu().numpy().copy())
+    torch.cuda.synchronize()
+    return np.concatenate(xs), np.concatenate(ys), sums.cpu().numpy()
+
+
+def _model(arch, dtype):
+    import raman_mi355x as R
+    m = R.MODELS[arch]()
+    m.load_state_dict(golden_state_dict(arch, "trained" if arch == "RRCDNet" else "synth"), strict=True)
+    return m.cuda().eval().set_engine_dtype(dtype)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "f16f8"])
+@pytest.mark.parametrize("arch", ["RRCDNet", "ADSDN"])
+def test_chunked_pipeline_equals_whole_batch(arch, dtype):
+    m = _model(arch, dtype)
+    xc, yc, sc = _pipeline(m, arch, dtype, n=6, chunk=2, L=1500)
+    xw, yw, sw = _pipeline(m, arch, dtype, n=6, chunk=6, L=1500)
+    assert np.array_equal(xc, xw)
+    assert np.array_equal(yc, yw)
+    assert sc[4] == sw[4] == 6
+    np.testing.assert_allclose(sc[:4], sw[:4], rtol=1e-12)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "f16f8"])
+def test_pipeline_matches_oracle(dtype):
+    from oracle.metrics import per_spectrum
+    from oracle.models import forward as oracle_forward
+    from raman_mi355x import engine
+    arch, L = "RRCDNet", 2000
+    m = _model(arch, dtype)
+    x, y, sums = _pipeline(m, arch, dtype, n=4, chunk=2, L=L, first=1000)
+    ref = oracle_forward(arch, golden_state_dict(arch, "trained"), torch.from_numpy(x).unsqueeze(1)).squeeze(1).numpy()
+    scale = max(np.abs(ref).max(), 1e-30)
+    err = np.abs(y - ref).max()
+    tol = 1e-5 * scale if dtype == "fp32" else 2e-2 * max(1.0, scale)
+    assert err <= tol, f"{dtype}: {err:.3e} > {tol:.3e}"
+    # metric sums of the pipeline vs the oracle's metrics on the pipeline's own outputs
+    clean, _, _, _ = engine.generate(4, SEED, first_index=1000, signal_length=L, device="cuda")
+    ref_sums = per_spectrum(y, clean.cpu().numpy()).sum(axis=0)
+    np.testing.assert_allclose(sums[:4], ref_sums, rtol=1e-10, atol=1e-12)
+    assert sums[4] == 4
