@@ -204,3 +204,32 @@ def test_cbam_team_matches_segment_path(arch, monkeypatch):
     monkeypatch.delenv("RDN_CBAM_SEGMENTS")
     scale = max(np.abs(y_seg).max(), 1e-30)
     assert np.abs(y_team - y_seg).max() <= 2e-6 * scale, np.abs(y_team - y_seg).max() / scale
+
+
+# halo rows per side of the 640-row fused tiles (csrc/common.hpp fused_halo)
+SHORT_TILE_HALO = {"DenoiseCNN": 20, "RRCDNet": 29, "PIDN": 32}
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "f16f8"])
+@pytest.mark.parametrize("arch", list(SHORT_TILE_HALO))
+@pytest.mark.parametrize("need", [256, 257, 384, 385, 512, 513])
+@pytest.mark.parametrize("tiles", [1, 3])
+def test_short_last_tile_boundaries(arch, need, tiles, dtype):
+    """The last tile runs on the fewest 128-row blocks reaching position L + 1 (need = L - base + 2
+    rows; csrc/fused_inplace.hip): lengths at each block-count boundary, as the only tile and as the
+    third, against the CPU oracle."""
+    from oracle.models import forward as oracle_forward
+    H = SHORT_TILE_HALO[arch]
+    T = 640 - 2 * H
+    L = need - 2 + (tiles - 1) * T - H
+    if L < 1 or (L + T - 1) // T != tiles:
+        pytest.skip(f"need={need} is not reachable with {tiles} tile(s)")
+    sd = golden_state_dict(arch, "synth")
+    m = _model(arch, "synth", dtype)
+    x = np.random.default_rng(need + tiles).uniform(-0.2, 1.2, (2, L)).astype(np.float32)
+    y = _run(m, x)
+    ref = oracle_forward(arch, sd, torch.from_numpy(x).unsqueeze(1)).squeeze(1).numpy()
+    scale = max(np.abs(ref).max(), 1e-30)
+    err = np.abs(y - ref).max()
+    tol = F32_REL * scale if dtype == "fp32" else BF16_ABS * max(1.0, scale)
+    assert err <= tol, f"{arch} L={L} {dtype}: {err:.3e} > {tol:.3e}"
