@@ -17,7 +17,10 @@ namespace ip {
 // 128-row blocks per tile: 640-row tiles (the whole LDS, no guard rows) everywhere except DSDN,
 // whose ResidualBlock identity lives in VGPRs (20 vs 16 f32x4 per lane at 640 rows: spills).
 template <int ARCH> struct NetGeo { static constexpr int NBK = 5; };
-template <> struct NetGeo<DSDN> { static constexpr int NBK = 4; };
+#ifndef RDN_DSDN_NBK
+#define RDN_DSDN_NBK 4
+#endif
+template <> struct NetGeo<DSDN> { static constexpr int NBK = RDN_DSDN_NBK; };
 
 IP_BODY(denoisecnn) {
   constexpr int H = fused_halo(DENOISECNN);

@@ -22,7 +22,7 @@ VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "stamps_pre0": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_ID_PRE=0", "stamps_reload": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_RELOAD_A=1",
             "stamps_pre16": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_ID_PRE=16", "nobar": "-DRDN_ABLATE_NOBARRIER",
             "ntpipe": "-DRDN_IP_NTPIPE=1", "ntpipe0": "-DRDN_IP_NTPIPE=0", "fastsplit": "-DRDN_H8_FASTSPLIT=1",
-            "hibase0": "-DRDN_IP_HIBASE=0"}
+            "hibase0": "-DRDN_IP_HIBASE=0", "dsdn3": "-DRDN_DSDN_NBK=3"}
 
 
 def build():
@@ -62,7 +62,9 @@ def run():
     x = noisy.view(B, 1, L)
     y = torch.empty_like(x)
     torch.manual_seed(0)
-    model = R.RRCDNet()
+    arch = os.environ.get("RDN_ABLATE_ARCH", "RRCDNet")     # network to time (default RRCDNet)
+    aid = engine._arch(arch)
+    model = R.MODELS[arch]()
     libs = {}
     for name in VARIANTS:
         if not os.path.exists(os.path.join(OUT, f"lib_{name}.so")):
@@ -73,7 +75,7 @@ def run():
             getattr(lib, fn).restype = res
         libs[name] = lib
     results = {}
-    names = engine.param_names("RRCDNet")
+    names = engine.param_names(arch)
     sd = model.state_dict()
     host = [sd[k].detach().float().contiguous() for k in names]
     ptrs = (ctypes.c_void_p * len(host))(*[t.data_ptr() for t in host])
@@ -81,9 +83,9 @@ def run():
 
     def pack_with(lib, code):
         size = ctypes.c_size_t()
-        assert lib.rdn_packed_size(1, code, ctypes.byref(size)) == 0
+        assert lib.rdn_packed_size(aid, code, ctypes.byref(size)) == 0
         blob = torch.empty(size.value, dtype=torch.uint8)
-        rc = lib.rdn_pack(1, code, ptrs, numels, len(host), ctypes.c_void_p(blob.data_ptr()), size.value)
+        rc = lib.rdn_pack(aid, code, ptrs, numels, len(host), ctypes.c_void_p(blob.data_ptr()), size.value)
         assert rc == 0, lib.rdn_last_error()
         return blob.to(dev)
 
@@ -96,10 +98,10 @@ def run():
             for name, lib in libs.items():
                 stream = torch.cuda.current_stream().cuda_stream
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                lib.rdn_forward(1, code, packed[name].data_ptr(), x.data_ptr(), y.data_ptr(), B, L, None, 0, stream)
+                lib.rdn_forward(aid, code, packed[name].data_ptr(), x.data_ptr(), y.data_ptr(), B, L, None, 0, stream)
                 e0.record()
                 for _ in range(3):
-                    rc = lib.rdn_forward(1, code, packed[name].data_ptr(), x.data_ptr(), y.data_ptr(), B, L, None, 0, stream)
+                    rc = lib.rdn_forward(aid, code, packed[name].data_ptr(), x.data_ptr(), y.data_ptr(), B, L, None, 0, stream)
                     assert rc == 0, lib.rdn_last_error()
                 e1.record()
                 torch.cuda.synchronize()
