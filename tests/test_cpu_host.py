@@ -151,3 +151,19 @@ def test_metric_allreduce_world2_gloo():
     exp = per.mean(axis=0)
     for i, k in enumerate(("MSE", "SSIM", "Smoothness", "Peak2Peak")):
         assert abs(got[k] - exp[i]) <= 1e-12 * max(1.0, abs(exp[i]))
+
+
+def test_bench_algorithmic_flops_match_survey():
+    """bench.py's roofline numerator: sum over Conv1d layers of 2*Cin*Cout*K*L,
+    per spectrum at L = 10,000 and PIDN / APIDN at L = 16,384."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    survey = {"DenoiseCNN": 4.4314e9, "RRCDNet": 7.1424e9, "DSDN": 7.8720e9, "ADSDN": 7.8768e9,
+              "PIDN": 7.3805e9, "APIDN": 7.3847e9}
+    for arch, g in survey.items():
+        assert abs(bench.flops_per_spectrum(arch, 10000) - g) / g < 5e-5, arch
+    assert abs(bench.flops_per_spectrum("PIDN", 16384) - 12.092e9) / 12.092e9 < 5e-4
+    assert abs(bench.flops_per_spectrum("APIDN", 16384) - 12.099e9) / 12.099e9 < 5e-4
