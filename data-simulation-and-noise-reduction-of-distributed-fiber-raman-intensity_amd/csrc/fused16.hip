@@ -188,6 +188,20 @@ __device__ __forceinline__ void conv(Tile& tl, uint32_t src, uint32_t dst, int d
   for (int u = 0; u < 2; ++u) sa[u] = (int)dst + soff(r0, 4 * u + q);
   const int pos0 = tl.base + w * RW;
 
+  // Idle waves of a short last tile: every row of this wave lies at position >= L + 2, beyond the
+  // reach (d <= 2) of any row that matters, so it skips the layer (its dst rows are never read by
+  // a stored output: positions L, L + 1 are re-zeroed by the wave that owns them, and the wrapped
+  // taps of rows 0, 1 erode into the halo like any other edge).  Its SIMD partner wave then has the
+  // MFMA pipe to itself.  It still fetches the next layer's operands and meets the barrier.
+  if (EDGE && __builtin_amdgcn_readfirstlane(pos0) >= tl.L + 2) {
+    if (has_next) load_frags(tl, next, F);
+#pragma unroll
+    for (int n = 0; n < NT; ++n) out[n] = 0.f;
+    tl.layer += 1;
+    if (NM == 4) lds_barrier();
+    return;
+  }
+
   // bias (+ identity), ReLU, zero rows outside [0, L), round to bf16, store the 8 channels of
   // M-tiles 2u, 2u+1 as one 16-B slot
   auto epilogue = [&](int n, int u, const f32x4 (&acc)[NM]) {
