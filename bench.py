@@ -31,13 +31,13 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "denoised spectra/sec (node) RRCDNet bf16/fp32 at 1/2/4/8 GPU; % MFMA peak"
 # Dense MFMA peaks, MI355X_MICROARCH.md §Chip-level parameters (spec values)
-PEAK_TFLOPS = {"bf16": 2500.0, "bf16x3": 2500.0, "f16f8": 2500.0, "fp32": 157.3}
+PEAK_TFLOPS = {"bf16-unsafe": 2500.0, "bf16x3": 2500.0, "f16f8": 2500.0, "fp32": 157.3}
 # conv layer counts per network: (64->64 convs, stems, heads) — SURVEY.md §2 table
 LAYERS = {"DenoiseCNN": (18, 1, 1), "RRCDNet": (29, 2, 2), "DSDN": (32, 1, 1), "PIDN": (30, 1, 1),
           "ADSDN": (32, 1, 1), "APIDN": (30, 1, 1)}
 SA_CONVS = {"ADSDN": 17, "APIDN": 15}
 # MFMA cycles per product relative to one bf16 MFMA (v_mfma_f32_16x16x32_bf16 = 16 cycles per K=32)
-MFMA_COST = {"bf16": 1, "bf16x3": 3, "f16f8": 2}
+MFMA_COST = {"bf16-unsafe": 1, "bf16x3": 3, "f16f8": 2}
 
 
 def flops_per_spectrum(arch, L):
@@ -82,12 +82,12 @@ def traffic_per_spectrum(arch, dtype):
 
 def time_forward(engine, arch, dtype, packed, x, y, steps, warmup, stream):
     for _ in range(warmup):
-        engine.forward(arch, dtype, packed, x, out=y)
+        engine.forward(arch, dtype, packed, x, out=y, check=False)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(steps):
-        engine.forward(arch, dtype, packed, x, out=y)
+        engine.forward(arch, dtype, packed, x, out=y, check=False)
     e1.record(stream)
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / steps
@@ -107,7 +107,7 @@ def time_pipeline(engine, arch, dtype, packed, seed, first, B, L, steps, stream,
         engine.generate(B, seed, first_index=first + i * B, signal_length=L, device=dev, out=(clean, noisy))
 
     def fwd():
-        engine.forward(arch, dtype, packed, noisy.view(B, 1, L), out=y)
+        engine.forward(arch, dtype, packed, noisy.view(B, 1, L), out=y, check=False)
 
     def met():
         engine.metrics(y.view(B, L), clean, sums=sums, per_spectrum=False)
@@ -140,7 +140,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--arch", default="RRCDNet")
-    ap.add_argument("--dtype", default="f16f8", choices=["bf16", "bf16x3", "f16f8", "fp32"])
+    ap.add_argument("--dtype", default="f16f8", choices=["bf16-unsafe", "bf16x3", "f16f8", "fp32"])
     ap.add_argument("--batch", type=int, default=8192, help="spectra per GPU per step")
     ap.add_argument("--L", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=20250410)
@@ -173,7 +173,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     def step():
-        engine.forward(args.arch, args.dtype, packed, x, out=y)
+        engine.forward(args.arch, args.dtype, packed, x, out=y, check=False)
 
     for _ in range(args.warmup):
         step()
@@ -198,6 +198,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
+    # the timed launches ran unchecked (check=False); a failed CBAM hand-off would show as NaN here
+    if not bool(torch.isfinite(y).all()):
+        raise RuntimeError("non-finite outputs in the timed forward")
     # evaluation metrics of the last step, all-reduced across ranks (RCCL over xGMI) — untimed
     _, sums = engine.metrics(y.view(B, L), clean)
     if world > 1:
@@ -206,7 +209,7 @@ def main():
 
     variants = {}
     if not args.no_variants:
-        for dt in ("f16f8", "bf16x3", "bf16", "fp32"):
+        for dt in ("f16f8", "bf16x3", "bf16-unsafe", "fp32"):
             if dt == args.dtype:
                 continue
             nb = B if dt != "fp32" else max(1, B // 4)

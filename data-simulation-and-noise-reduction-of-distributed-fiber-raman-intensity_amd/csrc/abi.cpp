@@ -18,7 +18,8 @@ hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const 
 
 hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                void* ws, size_t ws_bytes, hipStream_t s);
-size_t cbam_workspace_bytes(int arch, int dtype, int64_t n, int64_t L);
+size_t cbam_workspace_bytes(int arch, int dtype, int64_t n, int64_t L, hipStream_t s);
+hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t s, int* timed_out);
 hipError_t launch_generate(uint64_t seed, uint64_t first, int64_t n, int L, float snr_lo, float snr_hi, float extreme_prob,
                            int max_repeat, float* clean, float* noisy, float* snr, float* nstd, hipStream_t s);
 hipError_t launch_metrics(const float* y, const float* clean, int64_t n, int L, double* per, double* sums, hipStream_t s);
@@ -56,7 +57,13 @@ bool is_cbam(int a) { return a == RDN_ADSDN || a == RDN_APIDN; }
 
 extern "C" {
 
+#ifndef RDN_SOURCE_HASH
+#define RDN_SOURCE_HASH "unstamped"
+#endif
+
 int rdn_version(void) { return RDN_ABI_VERSION; }
+
+const char* rdn_build_id(void) { return RDN_SOURCE_HASH; }
 
 const char* rdn_last_error(void) { return g_err.c_str(); }
 
@@ -105,7 +112,7 @@ int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes)
   RDN_GUARD_BEGIN
   if (!valid_arch(arch) || !valid_dtype(dtype) || !bytes || n < 0 || L < 1)
     return fail(RDN_EINVAL, "rdn_workspace_size: bad argument");
-  *bytes = is_cbam(arch) ? rdn::cbam_workspace_bytes(arch, dtype, n, L) : 0;
+  *bytes = is_cbam(arch) ? rdn::cbam_workspace_bytes(arch, dtype, n, L, nullptr) : 0;
   return RDN_OK;
   RDN_GUARD_END
 }
@@ -120,13 +127,30 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
   const hipStream_t s = (hipStream_t)stream;
   const uint8_t* blob = (const uint8_t*)packed;
   if (is_cbam(arch)) {
-    const size_t need = rdn::cbam_workspace_bytes(arch, dtype, n, L);
+    const size_t need = rdn::cbam_workspace_bytes(arch, dtype, n, L, s);
     if (ws_bytes < need || (need && !ws))
       return fail(RDN_ESIZE, "rdn_forward: workspace too small, need " + std::to_string(need) + " bytes");
     return hip_check(rdn::launch_cbam_forward(arch, dtype, blob, x, y, n, (int)L, ws, ws_bytes, s), "cbam forward");
   }
   if (dtype == RDN_BF16) return hip_check(rdn::launch_fused16(arch, blob, x, y, n, (int)L, s), "fused bf16 forward");
   return hip_check(rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, s), "fused in-place forward");
+  RDN_GUARD_END
+}
+
+int rdn_forward_status(int arch, int dtype, int64_t n, int64_t L, void* ws, size_t ws_bytes, void* stream) {
+  RDN_GUARD_BEGIN
+  if (!valid_arch(arch) || !valid_dtype(dtype)) return fail(RDN_EINVAL, "rdn_forward_status: unknown arch/dtype");
+  if (n < 0 || L < 1 || L > 0x7fffffff) return fail(RDN_EINVAL, "rdn_forward_status: bad n / L");
+  const hipStream_t s = (hipStream_t)stream;
+  if (!is_cbam(arch) || n == 0) return hip_check(hipStreamSynchronize(s), "rdn_forward_status");
+  int timed_out = 0;
+  const int rc = hip_check(rdn::cbam_status(arch, dtype, L, ws, ws_bytes, s, &timed_out), "rdn_forward_status");
+  if (rc != RDN_OK) return rc;
+  if (timed_out)
+    return fail(RDN_EHIP, "CBAM team hand-off timed out: a workgroup of a spectrum's team never arrived (the "
+                          "grid's co-residency was broken, e.g. by a concurrent kernel on the device); the "
+                          "affected spectra's outputs are NaN");
+  return RDN_OK;
   RDN_GUARD_END
 }
 

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "inplace.hpp"
+#include "host_util.hpp"
 
 namespace rdn {
 namespace cb {
@@ -255,8 +256,10 @@ __global__ __launch_bounds__(THREADS) void segment(const uint8_t* __restrict__ b
     stem<MODE, true>(tl, 0);
     __syncthreads();
   }
+  double d[HEAD_ROWS];
+  head<MODE>(tl, sg.head_slot, d);
   float v[HEAD_ROWS];
-  head<MODE>(tl, sg.head_slot, v);
+  round_rows(d, v);
   if (sg.head_sigmoid) {
 #pragma unroll
     for (int k = 0; k < HEAD_ROWS; ++k) v[k] = sigm(v[k]);
@@ -307,8 +310,9 @@ struct TeamArgs {
   char* slots;          // [teams][2][TT][SLOT_BYTES]
   unsigned* counters;   // [teams][TEAM_CTR_STRIDE], zeroed before the launch
   char* hsave;          // [teams * TT][WB][64] f32
-  unsigned* err;
+  unsigned* err;         // hand-off error word: set when a team wait times out (read by cbam_status)
   unsigned long long* stamps;   // RDN_TEAM_STAMPS diagnostics: [grid][NSTAMP] cycle sums per phase
+  int force_miss;       // test knob (RDN_CBAM_FORCE_MISS=k): workgroup 0 skips its k-th arrival
 };
 #ifndef RDN_TEAM_STAMPS
 #define RDN_TEAM_STAMPS 0
@@ -437,7 +441,8 @@ __device__ __forceinline__ void load8(const char* lds, int r, int k, float (&v)[
 
 // per-channel sum / max of u over the tile's own positions -> slot (sc1); arrive at the counter
 template <int MODE>
-__device__ __forceinline__ void publish_stats(const Tile& tl, const TeamArgs& ta, char* slot, unsigned* ctr, Stamps& st) {
+__device__ __forceinline__ void publish_stats(const Tile& tl, const TeamArgs& ta, char* slot, unsigned* ctr, Stamps& st,
+                                              bool arrive = true) {
   char* lds = tl.lds;
   const int tid = opaque_tid(), lane = tid & 63, w = tid >> 6, sub = lane & 15, rgrp = lane >> 4;
   const int H = ta.halo, T = ta.T;
@@ -496,17 +501,23 @@ __device__ __forceinline__ void publish_stats(const Tile& tl, const TeamArgs& ta
     __hip_atomic_store((double*)slot + c, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store((unsigned*)(slot + 512) + c, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every lane's slot stores have landed
-    if (c == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c == 0 && arrive) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-// the team has arrived at `target`: lane 0 polls (sc1), the workgroup barrier releases the rest
+// the team has arrived at `target`: lane 0 polls (sc1), the workgroup barrier releases the rest.
+// A wait that exceeds SPIN_LIMIT polls (a team member never arrived: the co-residency the grid is
+// sized for was broken, e.g. by a concurrent kernel) raises the error word and falls through; once
+// the word is up every later wait of every workgroup falls through at once, so the grid drains in
+// about one SPIN_LIMIT, the outputs of the affected spectra are NaN (team_forward) and the host
+// reports RDN_EHIP (cbam_status).
 __device__ __forceinline__ void team_wait(const TeamArgs& ta, unsigned* ctr, unsigned target) {
   if (__builtin_amdgcn_workitem_id_x() == 0) {
     unsigned it = 0;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(8);
-      if (++it > SPIN_LIMIT) {
+      if ((++it & 63) == 0 && __hip_atomic_load(ta.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+      if (it > SPIN_LIMIT) {
         __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -739,7 +750,8 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
     // next layer's operands are loaded only now (held across this VALU-heavy code they spill).
     auto cbam = [&](int slot, int res, bool save_next) {
       char* mine = tslots + ((size_t)(nbar & 1) * ta.TT + tile) * SLOT_BYTES;
-      publish_stats<MODE>(tl, ta, mine, ctr, stamp);
+      const bool skip = ta.force_miss > 0 && __builtin_amdgcn_workgroup_id_x() == 0 && nbar + 1 == (unsigned)ta.force_miss;
+      publish_stats<MODE>(tl, ta, mine, ctr, stamp, !skip);
       stamp(3);
       team_wait(ta, ctr, (nbar + 1) * (unsigned)ta.TT);
       stamp(4);
@@ -777,11 +789,19 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
       stem<MODE, true>(tl, 0);       // + h, recomputed from x
       __syncthreads();
     }
+    double d[HEAD_ROWS];
+    head<MODE>(tl, 1, d);
     float v[HEAD_ROWS];
-    head<MODE>(tl, 1, v);
+    round_rows(d, v);
     if (!ADS) {
 #pragma unroll
       for (int k = 0; k < HEAD_ROWS; ++k) v[k] = sigm(v[k]);
+    }
+    // a timed-out hand-off anywhere in the grid: this spectrum's CBAM statistics may be incomplete,
+    // so its outputs are NaN rather than plausible-looking garbage
+    if (__hip_atomic_load(ta.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+#pragma unroll
+      for (int k = 0; k < HEAD_ROWS; ++k) v[k] = __uint_as_float(0x7fc00000u);   // quiet NaN (bit pattern: -fno-honor-nans build)
     }
     store_out(tl, y, (int)n, v, ta.halo, ta.T);
     __syncthreads();                 // the next spectrum's stem overwrites the rows the head read
@@ -800,27 +820,46 @@ static constexpr int64_t CBAM_CHUNK = 1024;       // spectra per pass (bounds th
 static size_t act_bytes(int64_t n, int64_t L) { return (size_t)n * L * 64 * sizeof(float); }
 
 // Team-persistent geometry: TEAM_HALO rows per side (refreshed from the neighbours at every CBAM),
-// TT tiles per spectrum, as many teams as fit one workgroup per CU.
+// TT tiles per spectrum, as many teams as the device holds co-resident: the occupancy API's
+// workgroups per CU for this kernel (LDS-bound: 1) x the CUs of the stream's device.
 struct TeamGeo {
   int halo, T, TT, teams;
   size_t slots, counters, hsave, total;
 };
-static int device_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 0;
-  }
-  return cus;
+typedef void (*team_kernel_t)(const uint8_t*, const float*, float*, int, cb::TeamArgs);
+static team_kernel_t team_kernel(int arch, int mode) {
+  using namespace cb;
+  const bool ads = arch == ADSDN;
+  if (mode == ip::MODE_F32) return ads ? team_forward<ip::MODE_F32, true> : team_forward<ip::MODE_F32, false>;
+  if (mode == ip::MODE_X3) return ads ? team_forward<ip::MODE_X3, true> : team_forward<ip::MODE_X3, false>;
+  if (mode == ip::MODE_H8) return ads ? team_forward<ip::MODE_H8, true> : team_forward<ip::MODE_H8, false>;
+  return ads ? team_forward<ip::MODE_B1, true> : team_forward<ip::MODE_B1, false>;
 }
-static TeamGeo team_geo(int arch, int64_t L) {
+static int dtype_mode(int dtype) {
+  return dtype == F32 ? ip::MODE_F32 : dtype == BF16X3 ? ip::MODE_X3 : dtype == F16F8 ? ip::MODE_H8 : ip::MODE_B1;
+}
+// attribute slots 40-47 (team kernels) and 48-51 (segment kernels), host_util.hpp
+static int team_slot(int arch, int mode) { return 40 + 2 * mode + (arch == ADSDN); }
+
+// co-resident workgroups per CU of the team kernel on `dev` (0 on any failure)
+static int team_blocks_per_cu(int arch, int mode, int dev) {
+  const team_kernel_t k = team_kernel(arch, mode);
+  if (ensure_dynamic_lds((const void*)k, team_slot(arch, mode), (int)cb::SEG_LDS_BYTES, dev) != hipSuccess) return 0;
+  int cur = 0, nb = 0;
+  if (hipGetDevice(&cur) != hipSuccess) return 0;
+  if (cur != dev && hipSetDevice(dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k, THREADS, cb::SEG_LDS_BYTES) != hipSuccess) nb = 0;
+  if (cur != dev) (void)hipSetDevice(cur);
+  return nb;
+}
+
+static TeamGeo team_geo(int arch, int mode, int64_t L, int dev) {
   TeamGeo g{};
   g.halo = cb::TEAM_HALO;                  // halos refreshed from the neighbours at every CBAM
   g.T = WB - 2 * g.halo;
   g.TT = (int)((L + g.T - 1) / g.T);
-  const int cus = device_cus();
-  g.teams = cus > 0 ? cus / g.TT : 0;
+  const int resident = device_cus(dev) * team_blocks_per_cu(arch, mode, dev);
+  g.teams = resident > 0 ? resident / g.TT : 0;
   const char* env = getenv("RDN_CBAM_SEGMENTS");       // diagnostics: force the per-segment path
   if (env && env[0] == '1') g.teams = 0;
   if (g.teams > 0) {
@@ -832,32 +871,28 @@ static TeamGeo team_geo(int arch, int64_t L) {
   return g;
 }
 
-size_t cbam_workspace_bytes(int arch, int, int64_t n, int64_t L) {
-  const TeamGeo g = team_geo(arch, L);
+size_t cbam_workspace_bytes(int arch, int dtype, int64_t n, int64_t L, hipStream_t stream) {
+  const TeamGeo g = team_geo(arch, dtype_mode(dtype), L, stream_device(stream));
   if (g.teams > 0) return g.total;
   const int64_t c = n < CBAM_CHUNK ? n : CBAM_CHUNK;
   return 4 * act_bytes(c, L) + 2 * (size_t)c * 64 * (sizeof(double) + sizeof(unsigned)) + 256;
 }
 
+// workspace carve-up of the team kernel: slots | counters | identity buffers | error word | stamps
+static char* team_base(void* ws) { return (char*)(((uintptr_t)ws + 255) & ~(uintptr_t)255); }
+static char* team_hsave(const TeamGeo& g, void* ws) {
+  return team_base(ws) + ((g.slots + g.counters + 255) & ~(size_t)255);
+}
+static unsigned* team_err(const TeamGeo& g, void* ws) { return (unsigned*)(team_hsave(g, ws) + g.hsave); }
+
 // One launch for the whole network (see cb::team_forward).
 static hipError_t launch_team(int arch, int mode, const TeamGeo& g, const uint8_t* blob, const float* x, float* y,
                               int64_t n, int L, void* ws, hipStream_t stream) {
   using namespace cb;
-  typedef void (*team_kernel_t)(const uint8_t*, const float*, float*, int, TeamArgs);
-  const bool ads = arch == ADSDN;
-  team_kernel_t k;
-  if (mode == ip::MODE_F32) k = ads ? team_forward<ip::MODE_F32, true> : team_forward<ip::MODE_F32, false>;
-  else if (mode == ip::MODE_X3) k = ads ? team_forward<ip::MODE_X3, true> : team_forward<ip::MODE_X3, false>;
-  else if (mode == ip::MODE_H8) k = ads ? team_forward<ip::MODE_H8, true> : team_forward<ip::MODE_H8, false>;
-  else k = ads ? team_forward<ip::MODE_B1, true> : team_forward<ip::MODE_B1, false>;
-  static bool attr_set[4][2] = {};
-  const int mi = mode;                                 // MODE_* are 0..3
-  if (!attr_set[mi][ads]) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SEG_LDS_BYTES);
-    if (e != hipSuccess) return e;
-    attr_set[mi][ads] = true;
-  }
-  char* base = (char*)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
+  const team_kernel_t k = team_kernel(arch, mode);
+  const hipError_t ea = ensure_dynamic_lds((const void*)k, team_slot(arch, mode), (int)SEG_LDS_BYTES, stream_device(stream));
+  if (ea != hipSuccess) return ea;
+  char* base = team_base(ws);
   TeamArgs ta{};
   ta.TT = g.TT;
   ta.teams = g.teams;
@@ -866,8 +901,10 @@ static hipError_t launch_team(int arch, int mode, const TeamGeo& g, const uint8_
   ta.n = n;
   ta.slots = base;
   ta.counters = (unsigned*)(base + g.slots);
-  ta.hsave = base + ((g.slots + g.counters + 255) & ~(size_t)255);
-  ta.err = (unsigned*)(ta.hsave + g.hsave);
+  ta.hsave = team_hsave(g, ws);
+  ta.err = team_err(g, ws);
+  const char* miss = getenv("RDN_CBAM_FORCE_MISS");     // test knob: see TeamArgs::force_miss
+  ta.force_miss = miss ? atoi(miss) : 0;
   ta.stamps = cb::STAMP_BYTES ? (unsigned long long*)((char*)ws + g.total - cb::STAMP_BYTES) : nullptr;
   // counters and the error word start at 0 (the hand-off counts arrivals monotonically)
   hipError_t e = hipMemsetAsync(ta.counters, 0, g.counters, stream);
@@ -884,25 +921,21 @@ typedef void (*seg_kernel_t)(const uint8_t*, const float*, float*, int, int, int
 hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                void* ws, size_t ws_bytes, hipStream_t stream) {
   using namespace cb;
-  const int mode = dtype == F32 ? ip::MODE_F32 : dtype == BF16X3 ? ip::MODE_X3 : dtype == F16F8 ? ip::MODE_H8 : ip::MODE_B1;
+  const int mode = dtype_mode(dtype);
   const seg_kernel_t k = mode == ip::MODE_F32 ? segment<ip::MODE_F32>
                          : mode == ip::MODE_X3 ? segment<ip::MODE_X3>
                          : mode == ip::MODE_H8 ? segment<ip::MODE_H8> : segment<ip::MODE_B1>;
-  static bool attr_set[4] = {};
-  const int mi = mode;
-  if (!attr_set[mi]) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SEG_LDS_BYTES);
-    if (e != hipSuccess) return e;
-    attr_set[mi] = true;
-  }
-  const TeamGeo tg = team_geo(arch, L);
+  const int dev = stream_device(stream);
+  const hipError_t ea = ensure_dynamic_lds((const void*)k, 48 + mode, (int)SEG_LDS_BYTES, dev);
+  if (ea != hipSuccess) return ea;
+  const TeamGeo tg = team_geo(arch, mode, L, dev);
   if (tg.teams > 0) {
     if (ws_bytes < tg.total) return hipErrorInvalidValue;
     return launch_team(arch, mode, tg, blob, x, y, n, L, ws, stream);
   }
   const bool adsdn = arch == ADSDN;
   const int64_t chunk = n < CBAM_CHUNK ? n : CBAM_CHUNK;
-  if (ws_bytes < cbam_workspace_bytes(arch, dtype, chunk, L)) return hipErrorInvalidValue;
+  if (ws_bytes < cbam_workspace_bytes(arch, dtype, chunk, L, stream)) return hipErrorInvalidValue;
   char* base = (char*)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
   float* act[4];
   for (int i = 0; i < 4; ++i) act[i] = (float*)(base + i * act_bytes(chunk, L));
@@ -964,6 +997,21 @@ hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const f
       if (e != hipSuccess) return e;
     }
   }
+  return hipSuccess;
+}
+
+// After a CBAM forward on `stream`: wait for it and read the team kernel's hand-off error word.
+// *timed_out = 1 if a team wait exceeded its spin limit (outputs of affected spectra are NaN).
+hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t stream, int* timed_out) {
+  *timed_out = 0;
+  hipError_t e = hipStreamSynchronize(stream);
+  if (e != hipSuccess) return e;
+  const TeamGeo tg = team_geo(arch, dtype_mode(dtype), L, stream_device(stream));
+  if (tg.teams <= 0 || !ws || ws_bytes < tg.total) return hipSuccess;   // segment path: no hand-off
+  unsigned err = 0;
+  e = hipMemcpy(&err, team_err(tg, ws), sizeof(err), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  *timed_out = err != 0;
   return hipSuccess;
 }
 

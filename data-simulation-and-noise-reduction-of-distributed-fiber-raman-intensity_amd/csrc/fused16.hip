@@ -27,6 +27,7 @@
 // Reference forwards: 1DCNN/train.py:71-82, RRCDNet/train.py:72-98, DSDN/train.py:72-126,
 // PIDN/train.py:72-106.
 #include "common.hpp"
+#include "host_util.hpp"
 
 namespace rdn {
 namespace h16 {
@@ -447,12 +448,9 @@ hipError_t launch_fused16(int arch, const uint8_t* blob, const float* x, float* 
     case PIDN: k = h16::pidn; break;
     default: return hipErrorInvalidValue;
   }
-  static bool attr_set[8] = {};
-  if (!attr_set[arch]) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h16::LDS_BYTES);
-    if (e != hipSuccess) return e;
-    attr_set[arch] = true;
-  }
+  // attribute slots 0-7 (host_util.hpp)
+  const hipError_t e = ensure_dynamic_lds((const void*)k, arch, (int)h16::LDS_BYTES, stream_device(stream));
+  if (e != hipSuccess) return e;
   const int H = fused_halo(arch), T = h16::WB - 2 * H, tiles = (L + T - 1) / T;
   const int64_t chunk = (int64_t)(0x7fffffff / tiles);
   for (int64_t n0 = 0; n0 < n; n0 += chunk) {

@@ -4,6 +4,7 @@
 // Reference forwards: 1DCNN/train.py:71-82, RRCDNet/train.py:72-98, DSDN/train.py:72-126,
 // PIDN/train.py:72-106.
 #include "inplace.hpp"
+#include "host_util.hpp"
 
 namespace rdn {
 namespace ip {
@@ -32,8 +33,10 @@ IP_BODY(denoisecnn) {
   stem<MODE, false, NBK>(tl, 0);
   __syncthreads();
   for (int i = 0; i < 18; ++i) conv<MODE, RELU, G::S, EDGE, NBK>(tl, 1, id, a, i + 1 < 18);
+  double d[HEAD_ROWS];
+  head<MODE, NBK>(tl, 1, d);
   float o[HEAD_ROWS];
-  head<MODE, NBK>(tl, 1, o);
+  round_rows(d, o);
   store_out(tl, y, n, o, H, T);
 }
 
@@ -47,21 +50,22 @@ IP_BODY(rrcdnet) {
   stem<MODE, false, NBK>(tl, 0);
   __syncthreads();
   for (int i = 0; i < 15; ++i) conv<MODE, RELU, G::S, EDGE, NBK>(tl, 1, id, a, true);
-  float r[HEAD_ROWS];
+  double r[HEAD_ROWS];
   head<MODE, NBK>(tl, 2, r);
   __syncthreads();               // the left stem overwrites the rows the right head just read
   stem<MODE, false, NBK>(tl, 1);
   __syncthreads();
   for (int i = 0; i < 14; ++i) conv<MODE, RELU, G::S, EDGE, NBK>(tl, i == 7 ? 1 : 2, id, a, i + 1 < 14);
-  float l[HEAD_ROWS];
+  double l[HEAD_ROWS];
   head<MODE, NBK>(tl, 3, l);
+  float o[HEAD_ROWS];
 #pragma unroll
-  for (int k = 0; k < HEAD_ROWS; ++k) {
+  for (int k = 0; k < HEAD_ROWS; ++k) {      // x - (r + l)/2 from the unrounded heads, one rounding
     const int p = tl.base + (int)__builtin_amdgcn_workitem_id_x() + THREADS * k;
     const float xv = in_range(p, L) ? tl.x[p] : 0.f;
-    r[k] = xv - (r[k] + l[k]) / 2.0f;
+    o[k] = (float)((double)xv - (r[k] + l[k]) * 0.5);
   }
-  store_out(tl, y, n, r, H, T);
+  store_out(tl, y, n, o, H, T);
 }
 
 IP_BODY(dsdn) {
@@ -79,8 +83,10 @@ IP_BODY(dsdn) {
     conv<MODE, RELU, G::S, EDGE, NBK>(tl, 1, id, a, true);                      // relu(bn1(conv1 x))
     conv<MODE, RELU | ADD_ID | SAVE_ID, G::S, EDGE, NBK>(tl, 1, id, a, b < 14); // relu(bn2(conv2 .) + x)
   }
+  double d[HEAD_ROWS];
+  head<MODE, NBK>(tl, 1, d);
   float o[HEAD_ROWS];
-  head<MODE, NBK>(tl, 1, o);
+  round_rows(d, o);
   store_out(tl, y, n, o, H, T);
 }
 
@@ -99,8 +105,10 @@ IP_BODY(pidn) {
   }
   stem<MODE, true, NBK>(tl, 0);       // + identity (the stem output), recomputed from x
   __syncthreads();
+  double d[HEAD_ROWS];
+  head<MODE, NBK>(tl, 1, d);
   float o[HEAD_ROWS];
-  head<MODE, NBK>(tl, 1, o);
+  round_rows(d, o);
 #pragma unroll
   for (int k = 0; k < HEAD_ROWS; ++k) o[k] = 1.0f / (1.0f + expf(-o[k]));
   store_out(tl, y, n, o, H, T);
@@ -167,12 +175,9 @@ hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const 
   const int nbk = arch == DSDN ? ip::NetGeo<DSDN>::NBK : ip::NetGeo<RRCDNET>::NBK;
   const int wb = 128 * nbk;
   const uint32_t lds = nbk == 4 ? ip::TileGeo<4>::LDS : ip::TileGeo<5>::LDS;
-  static bool attr_set[4][8] = {};
-  if (!attr_set[dtype][arch]) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr_set[dtype][arch] = true;
-  }
+  // attribute slots 8-39 (host_util.hpp)
+  const hipError_t e = ensure_dynamic_lds((const void*)k, 8 + dtype * 8 + arch, (int)lds, stream_device(stream));
+  if (e != hipSuccess) return e;
   const int H = fused_halo(arch), T = wb - 2 * H, tiles = (L + T - 1) / T;
   const int64_t chunk = (int64_t)(0x7fffffff / tiles);
   for (int64_t n0 = 0; n0 < n; n0 += chunk) {

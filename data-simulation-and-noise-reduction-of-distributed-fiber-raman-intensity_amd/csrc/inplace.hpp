@@ -380,19 +380,21 @@ __device__ __forceinline__ void stem(const Tile& tl, int slot) {
 }
 
 // Conv1d(64, 1, 3, padding=1), one row per thread (row j = __builtin_amdgcn_workitem_id_x() + THREADS * k in out[k]),
-// fp32 weights and accumulate.
+// fp32 weights and activations, fp64 accumulate: the 192-term sum is exact to ~1e-16 and rounded
+// once by the caller, after the network's own combine (RRCDNet x - (r + l)/2, RRCDNet/train.py:98,
+// a cancellation; PIDN/APIDN sigmoid).  ~400 fp64 FMAs per thread per network: negligible.
 constexpr int HEAD_ROWS = 2;      // rows per thread: ceil(640 / 512)
 template <int MODE, int NBK = 4>
-__device__ __forceinline__ void head(const Tile& tl, int slot, float (&out)[HEAD_ROWS]) {
+__device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[HEAD_ROWS]) {
   using TG = TileGeo<NBK>;
   static_assert(TG::WB <= HEAD_ROWS * THREADS, "head rows per thread");
   const cfloat* hw = small_slot(tl, slot);
 #pragma unroll
   for (int k = 0; k < HEAD_ROWS; ++k) {
   const int j = opaque_tid() + THREADS * k;
-  out[k] = 0.f;
+  out[k] = 0.0;
   if (j >= TG::WB) continue;
-  float a = hw[192];
+  double a = (double)hw[192];
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
     const int prow = TG::row(j + t - 1);
@@ -400,11 +402,15 @@ __device__ __forceinline__ void head(const Tile& tl, int slot, float (&out)[HEAD
     for (int cb = 0; cb < 16; ++cb) {
       const f32x4 v = Op<MODE>::load4(tl.lds, prow, 4 * cb);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a = fmaf(hw[3 * (cb * 4 + i) + t], v[i], a);
+      for (int i = 0; i < 4; ++i) a = fma((double)hw[3 * (cb * 4 + i) + t], (double)v[i], a);
     }
   }
   out[k] = a;
   }
+}
+__device__ __forceinline__ void round_rows(const double (&d)[HEAD_ROWS], float (&f)[HEAD_ROWS]) {
+#pragma unroll
+  for (int k = 0; k < HEAD_ROWS; ++k) f[k] = (float)d[k];
 }
 
 // LDS-only workgroup barrier: waits for this wave's LDS traffic, NOT for its outstanding global
@@ -451,6 +457,34 @@ __device__ __forceinline__ void load_layer_a(const Tile& tl, int layer, LayerA<M
   }
 }
 
+// Compensated fp32 accumulation (MODE_F32): the exact-fp32 MFMA is a k-ordered fmaf chain, one
+// rounding per product, and over the 192-term reduction those roundings (not the fp32 storage of
+// the activations) dominate the error: a plain chain is ~8e-6 from the float64 forward on trained
+// RRCDNet, as far as the fp32 reference itself, so the two differ by up to 1.3e-5.  The chain is
+// therefore cut into chunks of RDN_F32_CHUNK k-steps (64 products); each chunk's sum is added to a
+// running total by an error-free TwoSum and the rounding error is injected as the next chunk's
+// accumulator start (no extra VGPRs over two plain partial sums).  CPU emulation of this exact
+// scheme: 4e-6 from the float64 forward (tools/precision_sweep.py --fp32).
+#ifndef RDN_F32_COMP
+#define RDN_F32_COMP 1
+#endif
+#ifndef RDN_F32_CHUNK
+#define RDN_F32_CHUNK 4
+#endif
+// hi + c = s + e exactly (Knuth TwoSum, 6 flops); hi <- s, c <- e.  Scalar ops on purpose (packed
+// f32 VALU next to MFMAs costs more than it saves, MI355X_MICROARCH.md cycle constants).
+__device__ __forceinline__ void two_sum(f32x4& hi, f32x4& c) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float a = hi[k], b = c[k];
+    const float s = a + b;
+    const float bb = s - a;
+    const float e = (a - (s - bb)) + (b - bb);
+    hi[k] = s;
+    c[k] = e;
+  }
+}
+
 // One Conv1d(64,64,3,d) over the tile, updated in place with a one-block lag.
 //
 // Block j reads input rows down to 128j - d, i.e. the tail of block j-1, so block j-1's outputs
@@ -475,6 +509,10 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   // bf16 modes start the accumulators at the folded bias; exact fp32 keeps the reference's
   // order (sum of products, then + bias) for its 1e-5 parity
   constexpr bool BIAS_INIT = MODE != MODE_F32;
+  constexpr bool COMP = MODE == MODE_F32 && RDN_F32_COMP && S == 0;   // S = 0: compensated chunks (two_sum)
+  constexpr int CH = RDN_F32_CHUNK;
+  constexpr int SP = COMP ? 1 : S;                           // MFMA accumulator sets
+  static_assert(!COMP || RDN_IP_NTPIPE, "compensated accumulation is implemented on the N-tile pipeline");
   f32x4 bias_l[MT];
   uint32_t sc_l[MT];
 #pragma unroll
@@ -540,7 +578,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
     const int row = rb + 16 * i + c16;
     const bool zero = !inside && !in_range(tl.base + row, tl.L);         // conv zero padding
     f32x4 v = res[j][i][mm];
-    if (!BIAS_INIT) v += bias_l[mm];
+    if (!BIAS_INIT && !COMP) v += bias_l[mm];
     if (EPI & ADD_ID) v += id[(j * NT + i) * MT + mm];
     if (EPI & RELU) v = __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
     if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -598,14 +636,21 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   for (int i = 0; i < NT; ++i) bnext[i] = read_b(0, 0, i);
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    f32x4 part[S][NT][MT];
+    f32x4 part[SP][NT][MT];
+    f32x4 hi[COMP ? NT : 1][COMP ? MT : 1];          // COMP: running total, starts at the bias
 #pragma unroll
-    for (int k = 0; k < S; ++k)
+    for (int k = 0; k < SP; ++k)
 #pragma unroll
       for (int i = 0; i < NT; ++i)
 #pragma unroll
         for (int mm = 0; mm < MT; ++mm)
           part[k][i][mm] = k == 0 && BIAS_INIT ? a.bias[mm] : f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (COMP) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int mm = 0; mm < MT; ++mm) hi[i][mm] = bias_l[mm];
+    }
     if (j == NB - 1 && has_next) {                    // last use of this layer's bias
 #pragma unroll
       for (int mm = 0; mm < MT; ++mm) a.bias[mm] = load_bias<MODE>(wnext, MT * mp + mm), a.sc[mm] = load_scale<MODE>(wnext, MT * mp + mm);
@@ -619,9 +664,26 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
 #pragma unroll
-        for (int mm = 0; mm < MT; ++mm) part[s % S][i][mm] = O::mma(a[mm][s], bnext[i], part[s % S][i][mm], sc_l[mm], s);
+        for (int mm = 0; mm < MT; ++mm) part[s % SP][i][mm] = O::mma(a[mm][s], bnext[i], part[s % SP][i][mm], sc_l[mm], s);
         if (s + 1 < O::KSTEPS) bnext[i] = read_b(j, s + 1, i);
         else if (j + 1 < NB) bnext[i] = read_b(j + 1, 0, i);
+        if constexpr (COMP) {
+          // fold a finished chunk into the running totals (the rounding error becomes the next
+          // chunk's accumulator start), staggered by one N-tile so that the VALU neither waits for
+          // the MFMAs it reads nor holds back the MFMAs that read it: N-tile i < NT-1 right after
+          // N-tile i+1's MFMAs of the chunk's last k-step, the last N-tile right after N-tile 0's
+          // MFMAs of the next k-step
+          const bool chunk_end = s % CH == CH - 1 && s + 1 < O::KSTEPS;
+          const bool chunk_next = s % CH == 0 && s > 0;
+          if (chunk_end && i > 0) {
+#pragma unroll
+            for (int mm = 0; mm < MT; ++mm) two_sum(hi[i - 1][mm], part[0][i - 1][mm]);
+          }
+          if (chunk_next && i == 0) {
+#pragma unroll
+            for (int mm = 0; mm < MT; ++mm) two_sum(hi[NT - 1][mm], part[0][NT - 1][mm]);
+          }
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
       if (j == NB - 1 && has_next) {                                   // last use of a[.][s]
@@ -664,9 +726,9 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #pragma unroll
         for (int mm = 0; mm < MT; ++mm) {
 #if defined(RDN_ABLATE_NOMFMA)
-          part[s % S][i][mm] += *(const f32x4*)&b;
+          part[s % SP][i][mm] += *(const f32x4*)&b;
 #else
-          part[s % S][i][mm] = O::mma(a[mm][s], b, part[s % S][i][mm], sc_l[mm], s);
+          part[s % SP][i][mm] = O::mma(a[mm][s], b, part[s % SP][i][mm], sc_l[mm], s);
 #endif
         }
       }
@@ -705,8 +767,12 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #pragma unroll
       for (int mm = 0; mm < MT; ++mm) {
         f32x4 v = part[0][i][mm];
+        if constexpr (COMP) {
+          v = hi[i][mm] + v;                          // total + last chunk (+ pending error): one rounding
+        } else {
 #pragma unroll
-        for (int k = 1; k < S; ++k) v += part[k][i][mm];
+          for (int k = 1; k < SP; ++k) v += part[k][i][mm];
+        }
         res[j][i][mm] = v;
       }
 #if defined(RDN_ABLATE_NOBARRIER)         // diagnostic builds only (tools/ablate.py): wrong results
@@ -721,11 +787,14 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   tl.layer += 1;
 }
 
-// partial sums per accumulator: F32 splits the fp32 chain 2 ways (128 accumulator VGPRs); the
-// residual net (DSDN) needs 64 VGPRs of identity and keeps one chain; split-bf16 error is
+// partial sums per accumulator (S = 0: one chain with compensated chunk sums, see two_sum): F32
+// compensates on the plain stacks (1DCNN, RRCDNet, PIDN; measured on the GPU with RDN_F32_CHUNK = 4:
+// trained RRCDNet 1.25e-5 -> 7.4e-6 vs the fp32 reference, 8.1e-6 -> 4.3e-6 vs float64, -8 %
+// throughput); the residual nets (DSDN, CBAM segments / teams) hold 64 VGPRs of identity and keep
+// one plain chain (compensation spills there: 159 VGPRs in DSDN); split-bf16 / f16f8 error is
 // dominated by the operand split, one chain.
 template <int MODE, bool RES> struct Geo { static constexpr int S = 1; };
-template <> struct Geo<MODE_F32, false> { static constexpr int S = 2; };
+template <> struct Geo<MODE_F32, false> { static constexpr int S = RDN_F32_COMP ? 0 : 2; };
 
 __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const float* x, int L, int T,
                                           int tiles, int halo, int& n_out) {

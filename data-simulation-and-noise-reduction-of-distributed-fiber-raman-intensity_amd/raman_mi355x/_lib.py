@@ -6,14 +6,34 @@ that device pointers and streams are shared with torch.  There is no fallback: i
 missing the import fails loudly.
 """
 import ctypes
+import glob
+import hashlib
 import os
 
 import torch  # noqa: F401  (must be loaded before the library, see module docstring)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libraman_mi355x.so")
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "lib", "libraman_mi355x.so")
+CSRC = os.path.join(os.path.dirname(PKG), "csrc")
+HEADER = os.path.join(os.path.dirname(os.path.dirname(PKG)), "include", "raman_mi355x.h")
 
 RDN_OK = 0
-ABI_VERSION = 1
+ABI_VERSION = 2
+
+
+def source_hash():
+    """sha256 prefix of the sources the library is built from -- the same files, in the same order,
+    as csrc/Makefile's STAMP_SRC (None when the sources are not beside the package)."""
+    if not os.path.isdir(CSRC):
+        return None
+    files = sorted(os.path.basename(p) for pat in ("*.hip", "*.cpp", "*.hpp")
+                   for p in glob.glob(os.path.join(CSRC, pat)))
+    paths = [os.path.join(CSRC, f) for f in files] + [os.path.join(CSRC, "Makefile"), HEADER]
+    h = hashlib.sha256()
+    for p in paths:
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_double_p = ctypes.POINTER(ctypes.c_double)
@@ -26,6 +46,9 @@ class GenParams(ctypes.Structure):
 
 _SIGNATURES = {
     "rdn_version": ([], ctypes.c_int),
+    "rdn_build_id": ([], ctypes.c_char_p),
+    "rdn_forward_status": ([ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                            ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
     "rdn_last_error": ([], ctypes.c_char_p),
     "rdn_param_names": ([ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "rdn_packed_size": ([ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
@@ -60,6 +83,10 @@ def lib():
             fn.restype = res
         if handle.rdn_version() != ABI_VERSION:
             raise ImportError(f"libraman_mi355x ABI {handle.rdn_version()} != expected {ABI_VERSION}")
+        built, tree = handle.rdn_build_id().decode(), source_hash()
+        if tree is not None and built != tree and os.environ.get("RDN_ALLOW_STALE_LIB") != "1":
+            raise ImportError(f"stale libraman_mi355x.so: built from sources {built}, this tree's sources hash to "
+                              f"{tree}; rebuild it (make -C csrc, or __graft_entry__.build())")
         _lib = handle
     return _lib
 

@@ -38,6 +38,7 @@ class _EngineNet(nn.Module):
         self._engine_dtype = "fp32"
         self._packed = None
         self._packed_key = None
+        self._tensor_cache = None
 
     # -- configuration -----------------------------------------------------------------------
     @property
@@ -45,19 +46,38 @@ class _EngineNet(nn.Module):
         return self._engine_dtype
 
     def set_engine_dtype(self, dtype):
-        """'fp32' (exact-fp32 MFMA, 1e-5 parity), 'bf16' (one bf16 MFMA per product, fastest) or
-        'bf16x3' (split-bf16, three bf16 MFMAs per product: bf16 speed class, ~1e-4 accuracy) or
-        'f16f8' (f16 product + one block-scaled e4m3 MFMA for both correction terms, ~1e-3 accuracy
-        at 2/3 of bf16x3's MFMA cycles)."""
+        """Arithmetic of the 64->64 convolutions:
+        'fp32'        exact-fp32 MFMA with compensated accumulation: within 1e-5 of the fp32 reference;
+        'f16f8'       f16 product + one block-scaled e4m3 MFMA carrying both correction terms (~15
+                      significant bits): within 2e-2 (measured <= 1e-3);
+        'bf16x3'      split bf16, three bf16 MFMAs per product: within 2e-2 (measured <= 6e-4);
+        'bf16-unsafe' one bf16 rounding per operand: fastest, NO tolerance guarantee (0.24 on trained
+                      RRCDNet).  Plain 'bf16' is refused (engine._dtype)."""
         code = engine._dtype(dtype)
-        self._engine_dtype = {0: "fp32", 1: "bf16", 2: "bf16x3", 3: "f16f8"}[code]
+        self._engine_dtype = engine.DTYPE_NAME[code]
         return self
 
     # -- packing -----------------------------------------------------------------------------
+    def _slots(self):
+        """(owner dict, name, tensor) of every parameter and buffer, cached: the pack key below is
+        rebuilt on every forward (the reference evaluate loop is batch-1, evaulate.py:29-32), and
+        rebuilding state_dict() there costs more than a small forward.  The cache is re-derived
+        whenever any slot no longer holds the tensor it recorded (a parameter or buffer replaced
+        anywhere in the tree, .to() / _apply swapping storages)."""
+        c = self._tensor_cache
+        if c is None or any(d.get(k) is not t for d, k, t in c):
+            c = []
+            for mod in self.modules():
+                for d in (mod._parameters, mod._buffers):
+                    c.extend((d, k, t) for k, t in d.items() if t is not None)
+            self._tensor_cache = c
+        return c
+
     def _state_key(self, device):
-        sd = self.state_dict(keep_vars=True)
+        # identity + storage + version counter of each tensor: in-place updates (optimizer steps,
+        # .add_(), load_state_dict's copy_) bump _version; replacements change identity or storage
         return (str(device), self._engine_dtype,
-                tuple((t.data_ptr(), t._version) for t in sd.values() if torch.is_tensor(t)))
+                tuple((t.data_ptr(), t._version) for _, _, t in self._slots()), len(self._tensor_cache))
 
     def packed_weights(self, device):
         key = self._state_key(device)

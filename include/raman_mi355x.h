@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RDN_ABI_VERSION 1
+#define RDN_ABI_VERSION 2
 
 typedef enum {
   RDN_DENOISECNN = 0, /* 1DCNN/train.py   class DenoiseCNN */
@@ -44,9 +44,12 @@ typedef enum {
   RDN_APIDN = 5       /* APIDN/train.py   class APIDN      */
 } rdn_arch;
 
-/* Arithmetic of the 64->64 convolutions (stems, heads, bias, activations math: fp32 always).
- *   RDN_F32    exact-fp32 MFMA, fp32 activations               (1e-5 parity mode)
- *   RDN_BF16   one bf16 MFMA per product, bf16 activations      (fastest)
+/* Arithmetic of the 64->64 convolutions (stems, activations math: fp32; heads: fp32 operands,
+ * fp64 accumulation, one final rounding).
+ *   RDN_F32    exact-fp32 MFMA, fp32 activations, compensated (chunked TwoSum) accumulation
+ *                                                               (1e-5 parity mode)
+ *   RDN_BF16   one bf16 MFMA per product, bf16 activations: NO tolerance guarantee (misses the
+ *              2e-2 bf16 bar on trained RRCDNet: 0.24); the Python layer names it 'bf16-unsafe' 
  *   RDN_BF16X3 split bf16: operands as bf16 hi+lo pairs, three bf16 MFMAs per product
  *              (hi*hi + hi*lo + lo*hi), ~16-bit operands        (bf16 MFMA at 2e-2-safe accuracy)
  *   RDN_F16F8  f16 main product (v = hi + lo, hi = f16(v)) plus both correction products
@@ -66,6 +69,9 @@ enum {
 
 /* ABI version (RDN_ABI_VERSION) of the loaded library. */
 int rdn_version(void);
+
+/* Build stamp: sha256 prefix of the sources this library was compiled from (csrc/Makefile). */
+const char* rdn_build_id(void);
 
 /* Message of the last failing call on this thread ("" if none). */
 const char* rdn_last_error(void);
@@ -91,6 +97,15 @@ int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes)
  * (N,L) contiguous); packed: device copy of the rdn_pack blob; stream: hipStream_t or NULL. */
 int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* y, int64_t n, int64_t L,
                 void* workspace, size_t workspace_bytes, void* stream);
+
+/* Completion status of the rdn_forward last enqueued on `stream` with these arguments and this
+ * workspace: waits for the stream (hipStreamSynchronize), then, for the CBAM networks (ADSDN,
+ * APIDN), reads the team kernel's hand-off error word from the workspace.  RDN_EHIP if a team wait
+ * timed out (co-residency broken by a concurrent kernel; the affected spectra's outputs are NaN) or
+ * the stream reported an error; RDN_OK otherwise.  Replaces nothing in the reference (its forward
+ * is synchronous PyTorch); the Python module calls it after every CBAM forward. */
+int rdn_forward_status(int arch, int dtype, int64_t n, int64_t L, void* workspace, size_t workspace_bytes,
+                       void* stream);
 
 /* Simulator parameters; defaults of 数据集产生.py:5-7 are {10000, 20, 37, 0.05, 40}. */
 typedef struct {

@@ -42,7 +42,7 @@ from oracle.weights import synth_state_dict  # noqa: E402
 SEED_DATA = 20250410
 SEED_W = 1234
 ARCHS = ["DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN"]
-TRAINED = ["RRCDNet", "DenoiseCNN", "PIDN"]
+TRAINED = ["RRCDNet", "DenoiseCNN", "PIDN", "DSDN", "ADSDN", "APIDN"]
 # 64->64 conv gain of the synthetic weights: keeps the deep residual stacks finite and the Sigmoid
 # heads out of saturation (measured output std 0.02-0.6 at these settings).
 GAIN = {"DenoiseCNN": 1.0, "RRCDNet": 1.0, "DSDN": 0.7, "ADSDN": 1.0, "PIDN": 0.85, "APIDN": 0.85}

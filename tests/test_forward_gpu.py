@@ -1,18 +1,14 @@
 """Parity of the HIP forward against the reference's own outputs (golden fixtures) and the CPU oracle.
 
-Bars (BASELINE.json north_star):
-  fp32:   max|y - ref| / max|ref| <= 1e-5 (ref = the reference's fp32 CPU forward).  Where the fp32
-          reference is itself that far from the exact forward (the fixture's ``f64_*`` outputs: the
-          same reference modules run in float64) — trained RRCDNet, whose output is a cancellation
-          x - (r + l)/2, sits 5e-6..8e-6 from it — the bar is its rounding floor; there the engine must
-          be at least as close to the float64 forward as the reference is, and within 2e-5 of it.
-  bf16x3: max|y - ref| <= 2e-2 on normalised-intensity outputs (trained weights); for the synthetic
-          weight sets, whose outputs are not normalised, 2e-2 * max(1, max|ref|).  This is the bf16
-          MFMA mode that carries the 2e-2 claim.
-  f16f8:  same bar as bf16x3 (the f16 + e4m3-correction mode).
-  bf16:   single-rounding bf16 is NOT within 2e-2 on trained RRCDNet (0.22 measured; CPU emulation
-          tools/precision_sweep.py gives 0.20), so its test pins the documented error envelope
-          instead: max-abs <= 0.3 * max(1, max|ref|).
+Bars (BASELINE.json north_star), asserted as written:
+  fp32:   max|y - ref| / max|ref| <= 1e-5 (ref = the reference's fp32 CPU forward), every network,
+          every weight set, every input set.  (The engine's fp32 mode uses compensated chunked
+          accumulation and fp64 heads so that it sits well inside the fp32 reference's own
+          distance from the float64 forward, inplace.hpp two_sum.)
+  f16f8 / bf16x3: max|y - ref| <= 2e-2 on normalised-intensity outputs (trained weights); for the
+          synthetic weight sets, whose outputs are not normalised, 2e-2 * max(1, max|ref|).
+Plain single-rounding bf16 ('bf16-unsafe') carries no tolerance claim and is not tested here; its
+measured error envelope lives in tests/test_diagnostics_gpu.py.
 """
 import numpy as np
 import pytest
@@ -23,10 +19,8 @@ from conftest import INPUT_SETS, golden_state_dict, input_array, load_golden
 pytestmark = pytest.mark.gpu
 
 FUSED = ["DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN"]
-TRAINED = ["DenoiseCNN", "RRCDNet", "PIDN"]
 F32_REL = 1e-5
 BF16_ABS = 2e-2
-BF16_PLAIN_ENVELOPE = 0.3
 
 
 def _model(arch, which, dtype):
@@ -45,23 +39,28 @@ def _run(m, x_np):
     return y.squeeze(1).cpu().numpy()
 
 
+def _has_trained(arch):
+    return any(k.startswith("w::") for k in load_golden(arch).files)
+
+
 def _cases(archs):
     out = []
     for a in archs:
         out.append((a, "synth"))
-        if a in TRAINED:
+        if _has_trained(a):
             out.append((a, "trained"))
     return out
 
 
 def fp32_verdict(y, ref, exact):
-    """(ok, message) for the fp32 bar described in the module docstring."""
+    """(ok, message): max-relative error against the reference fp32 forward <= 1e-5.  The distances of
+    engine and reference from the float64 forward are reported, not used."""
     scale = max(np.abs(ref).max(), 1e-30)
     rel = np.abs(y - ref).max() / scale
     ours = np.abs(y - exact).max() / scale
     theirs = np.abs(ref - exact).max() / scale
     msg = f"vs ref {rel:.2e}; vs float64 forward: engine {ours:.2e}, reference {theirs:.2e}"
-    return rel <= F32_REL or (ours <= theirs and rel <= 2 * F32_REL), msg
+    return rel <= F32_REL, msg
 
 
 @pytest.mark.parametrize("arch,which", _cases(FUSED))
@@ -104,22 +103,7 @@ def test_f16f8_within_tolerance(arch, which, inputs):
         assert err <= tol, f"{arch}/{which}/{name}: f16f8 max-abs error {err:.3e} > {tol:.1e}"
 
 
-@pytest.mark.parametrize("arch,which", _cases(FUSED))
-def test_bf16_error_envelope(arch, which, inputs):
-    g = load_golden(arch)
-    m = _model(arch, which, "bf16")
-    for name in INPUT_SETS:
-        ref = g[f"{which}_{name}"]
-        y = _run(m, input_array(inputs, name))
-        err = np.abs(y - ref).max()
-        tol = BF16_PLAIN_ENVELOPE * max(1.0, float(np.abs(ref).max()))
-        print(f"{arch}/{which}/{name}: bf16 max-abs {err:.3e} (envelope {tol:.1e}, 2e-2 bar: "
-              f"{'met' if err <= BF16_ABS * max(1.0, float(np.abs(ref).max())) else 'NOT met'})")
-        assert np.isfinite(y).all()
-        assert err <= tol, f"{arch}/{which}/{name}: bf16 max-abs error {err:.3e} > {tol:.1e}"
-
-
-@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "bf16", "f16f8"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16x3", "f16f8"])
 @pytest.mark.parametrize("arch", FUSED)
 @pytest.mark.parametrize("L", [1, 2, 5, 453, 454, 455, 908, 2049])
 def test_ragged_lengths_vs_oracle(arch, L, dtype):
@@ -133,14 +117,13 @@ def test_ragged_lengths_vs_oracle(arch, L, dtype):
     ref = oracle_forward(arch, sd, torch.from_numpy(x).unsqueeze(1)).squeeze(1).numpy()
     scale = max(np.abs(ref).max(), 1e-30)
     err = np.abs(y - ref).max()
-    tol = {"fp32": F32_REL * scale, "bf16x3": BF16_ABS * max(1.0, scale), "f16f8": BF16_ABS * max(1.0, scale),
-           "bf16": BF16_PLAIN_ENVELOPE * max(1.0, scale)}[dtype]
+    tol = {"fp32": F32_REL * scale, "bf16x3": BF16_ABS * max(1.0, scale), "f16f8": BF16_ABS * max(1.0, scale)}[dtype]
     assert err <= tol, f"{arch} L={L} {dtype}: {err:.3e} > {tol:.3e}"
 
 
 def test_batch_independence_and_determinism():
     """Each spectrum's output is independent of its batch neighbours and bitwise reproducible."""
-    m = _model("RRCDNet", "trained", "bf16")
+    m = _model("RRCDNet", "trained", "f16f8")
     rng = np.random.default_rng(0)
     x = rng.uniform(0, 1, (7, 3000)).astype(np.float32)
     y_all = _run(m, x)
@@ -190,6 +173,28 @@ def test_cbam_team_halo_exchange(arch, L, dtype):
     err = np.abs(y - ref).max()
     tol = F32_REL * scale if dtype == "fp32" else BF16_ABS * max(1.0, scale)
     assert err <= tol, f"{arch} L={L} {dtype}: {err:.3e} > {tol:.3e}"
+
+
+@pytest.mark.parametrize("arch", ["ADSDN", "APIDN"])
+def test_cbam_team_timeout_is_reported(arch, monkeypatch):
+    """A team member that never arrives at a CBAM hand-off (RDN_CBAM_FORCE_MISS=k: workgroup 0 skips
+    its k-th arrival) must not yield plausible outputs with RDN_OK: rdn_forward_status reports
+    RDN_EHIP, the module raises, and the affected spectra are NaN."""
+    import raman_mi355x as R
+    from raman_mi355x import _lib, engine
+    m = _model(arch, "synth", "f16f8")
+    x = torch.from_numpy(np.random.default_rng(5).uniform(0, 1, (2, 1, 1200)).astype(np.float32)).cuda()
+    monkeypatch.setenv("RDN_CBAM_FORCE_MISS", "3")
+    with pytest.raises(_lib.EngineError, match="timed out"):
+        with torch.no_grad():
+            m(x)
+    y = engine.forward(arch, "f16f8", m.packed_weights(x.device), x, check=False)
+    torch.cuda.synchronize()
+    assert torch.isnan(y[0]).any()
+    monkeypatch.delenv("RDN_CBAM_FORCE_MISS")
+    with torch.no_grad():
+        y = m(x)                               # the next forward starts from a clean error word
+    assert torch.isfinite(y).all()
 
 
 @pytest.mark.parametrize("arch", ["ADSDN", "APIDN"])

@@ -22,20 +22,23 @@ VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "stamps_pre0": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_ID_PRE=0", "stamps_reload": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_RELOAD_A=1",
             "stamps_pre16": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_ID_PRE=16", "nobar": "-DRDN_ABLATE_NOBARRIER",
             "ntpipe": "-DRDN_IP_NTPIPE=1", "ntpipe0": "-DRDN_IP_NTPIPE=0", "fastsplit": "-DRDN_H8_FASTSPLIT=1",
-            "hibase0": "-DRDN_IP_HIBASE=0", "dsdn3": "-DRDN_DSDN_NBK=3"}
+            "hibase0": "-DRDN_IP_HIBASE=0", "dsdn3": "-DRDN_DSDN_NBK=3", "comp0": "-DRDN_F32_COMP=0",
+            "chunk1": "-DRDN_F32_CHUNK=1", "chunk3": "-DRDN_F32_CHUNK=3", "chunk4": "-DRDN_F32_CHUNK=4"}
 
 
 def build():
+    """Compile every requested variant (all objects in parallel, 8 jobs), then link each."""
     import torch
+    from concurrent.futures import ThreadPoolExecutor
     tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
     os.makedirs(OUT, exist_ok=True)
     srcs = ["fused16.hip", "fused_inplace.hip", "cbam.hip", "generator.hip", "metrics.hip", "abi.cpp",
             "pack.cpp"]
     only = sys.argv[2:]
-    for name, flag in VARIANTS.items():
-        if only and name not in only:
-            continue
-        objs = []
+    names = [n for n in VARIANTS if not only or n in only]
+    jobs = []
+    for name in names:
+        flag = VARIANTS[name]
         for s in srcs:
             o = os.path.join(OUT, f"{name}_{s}.o")
             cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mcode-object-version=5",
@@ -44,8 +47,14 @@ def build():
                 cmd += ["-fno-honor-nans", "-mno-amdgpu-ieee"]
             if s == "generator.hip":
                 cmd += ["-ffp-contract=off"]
-            subprocess.run(cmd, check=True, cwd=CSRC)
-            objs.append(o)
+            jobs.append(cmd)
+    with ThreadPoolExecutor(int(os.environ.get("ABLATE_JOBS", "8"))) as ex:
+        for r in ex.map(lambda c: subprocess.run(c, cwd=CSRC, capture_output=True, text=True), jobs):
+            if r.returncode:
+                print(r.stderr[-3000:])
+                raise SystemExit("compile failed")
+    for name in names:
+        objs = [os.path.join(OUT, f"{name}_{s}.o") for s in srcs]
         subprocess.run(["g++", "-shared", "-o", os.path.join(OUT, f"lib_{name}.so")] + objs +
                        [f"-L{tlib}", "-l:libamdhip64.so", f"-Wl,-rpath,{tlib}"], check=True)
         print("built", name, flush=True)
@@ -71,6 +80,8 @@ def run():
             continue
         lib = ctypes.CDLL(os.path.join(OUT, f"lib_{name}.so"))
         for fn, (args, res) in _lib._SIGNATURES.items():
+            if not hasattr(lib, fn):
+                continue
             getattr(lib, fn).argtypes = args
             getattr(lib, fn).restype = res
         libs[name] = lib
@@ -116,5 +127,64 @@ def run():
                   flush=True)
 
 
+def parity():
+    """Max error of every built variant against the golden fixtures (reference fp32 outputs and the
+    float64 forward), per network and weight set:  python tools/ablate.py parity fp32 [archs...]"""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fiber-raman-intensity_amd"))
+    from conftest import INPUT_SETS, golden_inputs, golden_state_dict, input_array, load_golden
+    from raman_mi355x import _lib, engine
+    dev = torch.device("cuda")
+    dtype = sys.argv[2] if len(sys.argv) > 2 else "fp32"
+    archs = sys.argv[3:] or ["RRCDNet", "DenoiseCNN", "PIDN", "DSDN", "ADSDN", "APIDN"]
+    code = engine.DTYPE_ID[dtype]
+    inp = golden_inputs()
+    for name in VARIANTS:
+        path = os.path.join(OUT, f"lib_{name}.so")
+        if not os.path.exists(path):
+            continue
+        lib = ctypes.CDLL(path)
+        for fn, (args, res) in _lib._SIGNATURES.items():
+            if not hasattr(lib, fn):
+                continue
+            getattr(lib, fn).argtypes = args
+            getattr(lib, fn).restype = res
+        for arch in archs:
+            aid = engine._arch(arch)
+            g = load_golden(arch)
+            for which in ["synth", "trained"]:
+                if which == "trained" and not any(k.startswith("w::") for k in g.files):
+                    continue
+                sd = golden_state_dict(arch, which)
+                names = engine.param_names(arch)
+                host = [sd[k].detach().float().contiguous() for k in names]
+                ptrs = (ctypes.c_void_p * len(host))(*[t.data_ptr() for t in host])
+                numels = (ctypes.c_int64 * len(host))(*[t.numel() for t in host])
+                size = ctypes.c_size_t()
+                assert lib.rdn_packed_size(aid, code, ctypes.byref(size)) == 0
+                blob = torch.empty(size.value, dtype=torch.uint8)
+                assert lib.rdn_pack(aid, code, ptrs, numels, len(host), ctypes.c_void_p(blob.data_ptr()), size.value) == 0
+                blob = blob.to(dev)
+                worst = [0.0, 0.0, 0.0]
+                for s_ in INPUT_SETS:
+                    xn = torch.from_numpy(np.ascontiguousarray(input_array(inp, s_))).to(dev)
+                    y = torch.empty_like(xn)
+                    wsz = ctypes.c_size_t()
+                    lib.rdn_workspace_size(aid, code, xn.shape[0], xn.shape[1], ctypes.byref(wsz))
+                    ws = torch.empty(max(1, wsz.value), dtype=torch.uint8, device=dev)
+                    rc = lib.rdn_forward(aid, code, blob.data_ptr(), xn.data_ptr(), y.data_ptr(), xn.shape[0], xn.shape[1],
+                                         ws.data_ptr(), wsz.value, torch.cuda.current_stream().cuda_stream)
+                    assert rc == 0, lib.rdn_last_error()
+                    yh = y.cpu().numpy()
+                    ref, ex = g[f"{which}_{s_}"], g[f"f64_{which}_{s_}"]
+                    sc = max(np.abs(ref).max(), 1e-30)
+                    worst = [max(worst[0], np.abs(yh - ref).max() / sc), max(worst[1], np.abs(yh - ex).max() / sc),
+                             max(worst[2], np.abs(ref - ex).max() / sc)]
+                print(f"{name:8s} {arch:10s} {which:7s} {dtype}: vs ref {worst[0]:.2e}  vs f64 {worst[1]:.2e}  "
+                      f"(ref vs f64 {worst[2]:.2e})", flush=True)
+
+
 if __name__ == "__main__":
-    {"build": build, "run": run}[sys.argv[1]]()
+    {"build": build, "run": run, "parity": parity}[sys.argv[1]]()
