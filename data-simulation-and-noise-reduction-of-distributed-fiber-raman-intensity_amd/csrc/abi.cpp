@@ -12,7 +12,11 @@
 namespace rdn {
 std::string pack(int arch, int dtype, const float* const* tensors, const int64_t* numels, int n, void* dst, size_t cap);
 size_t packed_bytes(const std::vector<Op>& spec, int dtype);
+void set_corr_mask(void* blob, uint64_t mask);
+uint64_t get_corr_mask(const void* blob);
+uint64_t f16mix_default_mask(int arch);
 hipError_t launch_fused16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
+hipError_t launch_fused16_f16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
 hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                 hipStream_t s);
 
@@ -40,7 +44,7 @@ int hip_check(hipError_t e, const char* what) {
 }
 
 bool valid_arch(int a) { return a >= RDN_DENOISECNN && a <= RDN_APIDN; }
-bool valid_dtype(int d) { return d == RDN_F32 || d == RDN_BF16 || d == RDN_BF16X3 || d == RDN_F16F8; }
+bool valid_dtype(int d) { return d >= RDN_F32 && d <= RDN_F16MIX; }
 bool is_cbam(int a) { return a == RDN_ADSDN || a == RDN_APIDN; }
 
 }  // namespace
@@ -108,6 +112,25 @@ int rdn_pack(int arch, int dtype, const float* const* tensors, const int64_t* nu
   RDN_GUARD_END
 }
 
+int rdn_default_correction_mask(int arch, uint64_t* mask) {
+  RDN_GUARD_BEGIN
+  if (!valid_arch(arch) || !mask) return fail(RDN_EINVAL, "rdn_default_correction_mask: bad argument");
+  *mask = rdn::f16mix_default_mask(arch);
+  return RDN_OK;
+  RDN_GUARD_END
+}
+
+int rdn_get_correction_mask(int arch, int dtype, const void* host_blob, size_t bytes, uint64_t* mask) {
+  RDN_GUARD_BEGIN
+  if (!valid_arch(arch) || !valid_dtype(dtype) || !host_blob || !mask)
+    return fail(RDN_EINVAL, "rdn_get_correction_mask: bad argument");
+  if (dtype != RDN_F16F8 && dtype != RDN_F16MIX) return fail(RDN_EINVAL, "rdn_get_correction_mask: not a correction layout");
+  if (bytes < rdn::packed_bytes(rdn::net_spec(arch), dtype)) return fail(RDN_ESIZE, "rdn_get_correction_mask: blob too small");
+  *mask = rdn::get_corr_mask(host_blob);
+  return RDN_OK;
+  RDN_GUARD_END
+}
+
 int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes) {
   RDN_GUARD_BEGIN
   if (!valid_arch(arch) || !valid_dtype(dtype) || !bytes || n < 0 || L < 1)
@@ -133,6 +156,9 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
     return hip_check(rdn::launch_cbam_forward(arch, dtype, blob, x, y, n, (int)L, ws, ws_bytes, s), "cbam forward");
   }
   if (dtype == RDN_BF16) return hip_check(rdn::launch_fused16(arch, blob, x, y, n, (int)L, s), "fused bf16 forward");
+  if (dtype == RDN_F16) return hip_check(rdn::launch_fused16_f16(arch, blob, x, y, n, (int)L, s), "fused f16 forward");
+  if (dtype == RDN_F16MIX && arch != RDN_RRCDNET)
+    return fail(RDN_EUNSUPPORTED, "RDN_F16MIX is built for RRCDNet; the other networks run RDN_F16");
   return hip_check(rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, s), "fused in-place forward");
   RDN_GUARD_END
 }

@@ -370,7 +370,10 @@ template <int MODE> struct IdRaw { typedef u32x4 T; };
 template <> struct IdRaw<MODE_H8> { typedef u32x3 T; };
 template <int MODE>
 __device__ __forceinline__ void id_store(char* lds, __amdgpu_buffer_rsrc_t hs, int r, int sub, f32x4 h) {
-  if (MODE == MODE_B1) *(bf16x4*)(lds + off_f32(r + GUARD, 128 + 8 * sub)) = __builtin_convertvector(h, bf16x4);
+  if constexpr (single16(MODE)) {
+    typedef typename Op<MODE>::V4 V4;
+    *(V4*)(lds + off_f32(r + GUARD, 128 + 8 * sub)) = __builtin_convertvector(h, V4);
+  }
   else if (MODE == MODE_H8) {
     const H8Split x = h8_split(h8_sat<false>(h));
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -393,8 +396,12 @@ __device__ __forceinline__ f32x4 id_value(typename IdRaw<MODE>::T v) {
 }
 template <int MODE>
 __device__ __forceinline__ f32x4 id_load(const char* lds, __amdgpu_buffer_rsrc_t hs, int r, int sub) {
-  if (MODE == MODE_B1) return __builtin_convertvector(*(const bf16x4*)(lds + off_f32(r + GUARD, 128 + 8 * sub)), f32x4);
-  return id_value<MODE>(id_fetch<MODE>(hs, r, sub));
+  if constexpr (single16(MODE)) {
+    typedef typename Op<MODE>::V4 V4;
+    return __builtin_convertvector(*(const V4*)(lds + off_f32(r + GUARD, 128 + 8 * sub)), f32x4);
+  } else {
+    return id_value<MODE>(id_fetch<MODE>(hs, r, sub));
+  }
 }
 
 // block input (all WB tile rows) -> identity (used after the stem; later blocks save it from the
@@ -427,6 +434,10 @@ __device__ __forceinline__ void load8(const char* lds, int r, int k, float (&v)[
       v[i] = a[i];
       v[4 + i] = b[i];
     }
+  } else if constexpr (MODE == MODE_F16) {
+    const h16x8_t hi = *(const h16x8_t*)(lds + off_f32(pr, 16 * k));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)hi[i];
   } else {
     const bf16x8 hi = *(const bf16x8*)(lds + off_f32(pr, 16 * k));
 #pragma unroll
@@ -653,7 +664,7 @@ __device__ __forceinline__ void apply_cbam(const Tile& tl, const TeamArgs& ta, c
   // -- identities of this thread's pointwise rows, in flight during the spatial pass
   const int sub = lane & 15, rgrp = lane >> 4;
   typename IdRaw<MODE>::T idr[ID_ITERS];
-  if (MODE != MODE_B1 && res != RES_NONE) {
+  if (!single16(MODE) && res != RES_NONE) {
 #pragma unroll
     for (int k = 0; k < ID_PRE<MODE>; ++k) idr[k] = id_fetch<MODE>(hs, pw_row<MODE>(w, rgrp, k), sub);
   }
@@ -705,7 +716,7 @@ __device__ __forceinline__ void apply_cbam(const Tile& tl, const TeamArgs& ta, c
 #pragma unroll
     for (int i = 0; i < 4; ++i) h[i] = (u[i] * cav[i]) * sr;
     if (res != RES_NONE) {
-      h += MODE == MODE_B1 || k >= ID_PRE<MODE> ? id_load<MODE>(lds, hs, r, sub) : id_value<MODE>(idr[k]);
+      h += single16(MODE) || k >= ID_PRE<MODE> ? id_load<MODE>(lds, hs, r, sub) : id_value<MODE>(idr[k]);
       if (res == RES_ADD_RELU) h = __builtin_elementwise_max(h, f32x4{0.f, 0.f, 0.f, 0.f});
     }
     const int p = tl.base + r;
@@ -744,6 +755,7 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
     tl.small = (const float*)blob;
     tl.big = blob + SMALL_BYTES;
     tl.layer = 0;
+    tl.corr = corr_mask(blob);
     LayerA<MODE> a;
     load_layer_a<MODE>(tl, 0, a);
     // stats of u -> team -> apply.  The identity rows are fetched while the team assembles; the
@@ -833,12 +845,14 @@ static team_kernel_t team_kernel(int arch, int mode) {
   if (mode == ip::MODE_F32) return ads ? team_forward<ip::MODE_F32, true> : team_forward<ip::MODE_F32, false>;
   if (mode == ip::MODE_X3) return ads ? team_forward<ip::MODE_X3, true> : team_forward<ip::MODE_X3, false>;
   if (mode == ip::MODE_H8) return ads ? team_forward<ip::MODE_H8, true> : team_forward<ip::MODE_H8, false>;
+  if (mode == ip::MODE_F16) return ads ? team_forward<ip::MODE_F16, true> : team_forward<ip::MODE_F16, false>;
   return ads ? team_forward<ip::MODE_B1, true> : team_forward<ip::MODE_B1, false>;
 }
 static int dtype_mode(int dtype) {
-  return dtype == F32 ? ip::MODE_F32 : dtype == BF16X3 ? ip::MODE_X3 : dtype == F16F8 ? ip::MODE_H8 : ip::MODE_B1;
+  return dtype == F32 ? ip::MODE_F32 : dtype == BF16X3 ? ip::MODE_X3 : dtype == F16F8 ? ip::MODE_H8
+       : dtype == F16 ? ip::MODE_F16 : ip::MODE_B1;
 }
-// attribute slots 40-47 (team kernels) and 48-51 (segment kernels), host_util.hpp
+// attribute slots 40-49 (team kernels) and 64-68 (segment kernels), host_util.hpp
 static int team_slot(int arch, int mode) { return 40 + 2 * mode + (arch == ADSDN); }
 
 // co-resident workgroups per CU of the team kernel on `dev` (0 on any failure)
@@ -924,9 +938,10 @@ hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const f
   const int mode = dtype_mode(dtype);
   const seg_kernel_t k = mode == ip::MODE_F32 ? segment<ip::MODE_F32>
                          : mode == ip::MODE_X3 ? segment<ip::MODE_X3>
-                         : mode == ip::MODE_H8 ? segment<ip::MODE_H8> : segment<ip::MODE_B1>;
+                         : mode == ip::MODE_H8 ? segment<ip::MODE_H8>
+                         : mode == ip::MODE_F16 ? segment<ip::MODE_F16> : segment<ip::MODE_B1>;
   const int dev = stream_device(stream);
-  const hipError_t ea = ensure_dynamic_lds((const void*)k, 48 + mode, (int)SEG_LDS_BYTES, dev);
+  const hipError_t ea = ensure_dynamic_lds((const void*)k, 64 + mode, (int)SEG_LDS_BYTES, dev);
   if (ea != hipSuccess) return ea;
   const TeamGeo tg = team_geo(arch, mode, L, dev);
   if (tg.teams > 0) {

@@ -32,6 +32,9 @@ constexpr int WAVES = THREADS / 64;
 constexpr int SMALL_SLOT_FLOATS = 256;
 constexpr int SMALL_SLOTS = 64;
 constexpr size_t SMALL_BYTES = SMALL_SLOTS * SMALL_SLOT_FLOATS * sizeof(float);   // 64 KiB
+// slot 63 word 0/1: 64-bit per-layer correction mask of the f16 + e4m3 layout (bit i = big layer i
+// consumes the e4m3 correction): all ones for RDN_F16F8, a calibrated subset for RDN_F16MIX
+constexpr int CORR_SLOT = 63;
 // bf16 big layer: A-fragments of v_mfma_f32_16x16x32_bf16, [m 4][kstep 6][lane 64][8 bf16],
 // lane l holds W[cout = 16m + (l&15)][cin = 32u + 8(l>>4) + j][tap t], kstep = 2t + u; then bias[64] f32.
 constexpr int BIG_FRAG_BYTES_BF16 = 4 * 6 * 64 * 16;                       // 24576
@@ -94,7 +97,7 @@ __device__ __forceinline__ uint32_t off_f32(int prow, int byte) {
 }
 
 enum Arch : int { DENOISECNN = 0, RRCDNET = 1, DSDN = 2, ADSDN = 3, PIDN = 4, APIDN = 5 };
-enum DType : int { F32 = 0, BF16 = 1, BF16X3 = 2, F16F8 = 3 };
+enum DType : int { F32 = 0, BF16 = 1, BF16X3 = 2, F16F8 = 3, F16 = 4, F16MIX = 5 };
 
 // receptive half-width (rows of halo needed on each side of a tile's outputs)
 __host__ __device__ constexpr int fused_halo(int arch) {

@@ -12,7 +12,7 @@ namespace ip {
 // Network bodies.  EDGE: the tile holds positions outside [0, L) (first / last tile of a
 // spectrum), whose rows every write-back re-zeroes; interior tiles skip that per-row select.
 #define IP_BODY(name) \
-  template <int MODE, bool EDGE, int NBK> \
+  template <int MODE, bool EDGE, int NBK, int TAIL> \
   __device__ __forceinline__ void name##_body(Tile& tl, float* y, int n, int L, int T)
 
 // 128-row blocks per tile: 640-row tiles (the whole LDS, no guard rows) everywhere except DSDN,
@@ -49,13 +49,28 @@ IP_BODY(rrcdnet) {
   if (NBK == 4) zero_guards(tl.lds);
   stem<MODE, false, NBK>(tl, 0);
   __syncthreads();
-  for (int i = 0; i < 15; ++i) conv<MODE, RELU, G::S, EDGE, NBK>(tl, 1, id, a, true);
+  if constexpr (TAIL == 0) {
+    for (int i = 0; i < 15; ++i) conv<MODE, RELU, G::S, EDGE, NBK>(tl, 1, id, a, true);
+  } else {
+    // RDN_F16MIX: plain f16 layers, the last one writing the e4m3 planes, then TAIL corrected layers
+    // (right_net.15-17 for TAIL = 3: the layers whose f16 rounding the head's cancellation
+    // x - (r + l)/2 amplifies most, tools/f16mix_select.py)
+    for (int i = 0; i < 14 - TAIL; ++i) conv<MODE, RELU, G::S, EDGE, NBK, false, false, false>(tl, 1, id, a, true);
+    conv<MODE, RELU, G::S, EDGE, NBK, false, true, true>(tl, 1, id, a, true);
+    for (int i = 0; i < TAIL; ++i) conv<MODE, RELU, G::S, EDGE, NBK, true, true, true>(tl, 1, id, a, true);
+  }
   double r[HEAD_ROWS];
   head<MODE, NBK>(tl, 2, r);
   __syncthreads();               // the left stem overwrites the rows the right head just read
   stem<MODE, false, NBK>(tl, 1);
   __syncthreads();
-  for (int i = 0; i < 14; ++i) conv<MODE, RELU, G::S, EDGE, NBK>(tl, i == 7 ? 1 : 2, id, a, i + 1 < 14);
+  if constexpr (TAIL == 0) {
+    for (int i = 0; i < 14; ++i) conv<MODE, RELU, G::S, EDGE, NBK>(tl, i == 7 ? 1 : 2, id, a, i + 1 < 14);
+  } else {
+    // plain f16; the last layer writes the e4m3 lo plane the head reads
+    for (int i = 0; i < 13; ++i) conv<MODE, RELU, G::S, EDGE, NBK, false, false, false>(tl, i == 7 ? 1 : 2, id, a, true);
+    conv<MODE, RELU, G::S, EDGE, NBK, false, true, false>(tl, 2, id, a, false);
+  }
   double l[HEAD_ROWS];
   head<MODE, NBK>(tl, 3, l);
   float o[HEAD_ROWS];
@@ -127,8 +142,11 @@ IP_BODY(pidn) {
 #ifndef RDN_IP_PRIO
 #define RDN_IP_PRIO 0
 #endif
+// RDN_F16MIX: corrected layers at the end of RRCDNet's right branch (pack.cpp f16mix_default_mask)
+constexpr int RRCDNET_F16MIX_TAIL = 3;
+
 #define IP_KERNEL(name, arch)                                                                              \
-  template <int MODE>                                                                                      \
+  template <int MODE, int TAIL = 0>                                                                         \
   __global__ __launch_bounds__(THREADS) void name(const uint8_t* __restrict__ blob, const float* __restrict__ x, \
                                                  float* __restrict__ y, int L, int T, int tiles) {          \
     extern __shared__ __attribute__((aligned(16))) char lds[];                                             \
@@ -137,11 +155,11 @@ IP_BODY(pidn) {
     if (RDN_IP_PRIO && __builtin_amdgcn_readfirstlane(__builtin_amdgcn_workitem_id_x()) >= 256) __builtin_amdgcn_s_setprio(1);  \
     constexpr int NBK = NetGeo<arch>::NBK;                                                                 \
     const int need = L - tl.base + 2;  /* rows up to position L + 1: short last tiles */                     \
-    if (tl.base >= 0 && tl.base + TileGeo<NBK>::WB <= L) name##_body<MODE, false, NBK>(tl, y, n, L, T);   \
-    else if (NBK == 5 && need <= 256) name##_body<MODE, true, NBK == 5 ? 2 : NBK>(tl, y, n, L, T);          \
-    else if (NBK == 5 && need <= 384) name##_body<MODE, true, NBK == 5 ? 3 : NBK>(tl, y, n, L, T);          \
-    else if (NBK == 5 && need <= 512) name##_body<MODE, true, NBK == 5 ? 4 : NBK>(tl, y, n, L, T);          \
-    else name##_body<MODE, true, NBK>(tl, y, n, L, T);                                                     \
+    if (tl.base >= 0 && tl.base + TileGeo<NBK>::WB <= L) name##_body<MODE, false, NBK, TAIL>(tl, y, n, L, T);   \
+    else if (NBK == 5 && need <= 256) name##_body<MODE, true, NBK == 5 ? 2 : NBK, TAIL>(tl, y, n, L, T);          \
+    else if (NBK == 5 && need <= 384) name##_body<MODE, true, NBK == 5 ? 3 : NBK, TAIL>(tl, y, n, L, T);          \
+    else if (NBK == 5 && need <= 512) name##_body<MODE, true, NBK == 5 ? 4 : NBK, TAIL>(tl, y, n, L, T);          \
+    else name##_body<MODE, true, NBK, TAIL>(tl, y, n, L, T);                                                     \
   }
 
 IP_KERNEL(denoisecnn, DENOISECNN)
@@ -167,16 +185,18 @@ static fused_kernel_t pick(int arch) {
 // dtype: F32 (exact fp32), BF16X3 (split bf16) or F16F8 (f16 + e4m3 correction); see common.hpp
 hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                 hipStream_t stream) {
-  if (arch < 0 || arch >= 8 || dtype < 0 || dtype >= 4) return hipErrorInvalidValue;
+  if (arch < 0 || arch >= 8 || dtype < 0 || dtype > F16MIX) return hipErrorInvalidValue;
   const fused_kernel_t k = dtype == BF16X3 ? pick<ip::MODE_X3>(arch)
                            : dtype == F16F8 ? pick<ip::MODE_H8>(arch)
+                           : dtype == F16MIX ? (arch == RRCDNET ? ip::rrcdnet<ip::MODE_H8, ip::RRCDNET_F16MIX_TAIL> : nullptr)
                            : dtype == F32   ? pick<ip::MODE_F32>(arch) : nullptr;
   if (!k) return hipErrorInvalidValue;
   const int nbk = arch == DSDN ? ip::NetGeo<DSDN>::NBK : ip::NetGeo<RRCDNET>::NBK;
   const int wb = 128 * nbk;
   const uint32_t lds = nbk == 4 ? ip::TileGeo<4>::LDS : ip::TileGeo<5>::LDS;
-  // attribute slots 8-39 (host_util.hpp)
-  const hipError_t e = ensure_dynamic_lds((const void*)k, 8 + dtype * 8 + arch, (int)lds, stream_device(stream));
+  // attribute slots 8-39 and 70-77 (RDN_F16MIX), host_util.hpp
+  const int slot = dtype == F16MIX ? 70 + arch : 8 + dtype * 8 + arch;
+  const hipError_t e = ensure_dynamic_lds((const void*)k, slot, (int)lds, stream_device(stream));
   if (e != hipSuccess) return e;
   const int H = fused_halo(arch), T = wb - 2 * H, tiles = (L + T - 1) / T;
   const int64_t chunk = (int64_t)(0x7fffffff / tiles);

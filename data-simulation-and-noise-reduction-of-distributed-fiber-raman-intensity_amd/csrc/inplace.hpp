@@ -23,7 +23,9 @@
 namespace rdn {
 namespace ip {
 
-constexpr int MODE_F32 = 0, MODE_B1 = 1, MODE_X3 = 2, MODE_H8 = 3;
+constexpr int MODE_F32 = 0, MODE_B1 = 1, MODE_X3 = 2, MODE_H8 = 3, MODE_F16 = 4;
+// single-plane 16-bit modes (one MFMA per product, one rounding per operand)
+__host__ __device__ constexpr bool single16(int mode) { return mode == MODE_B1 || mode == MODE_F16; }
 #ifndef RDN_IP_SPREAD_STORE
 #define RDN_IP_SPREAD_STORE 1
 #endif
@@ -66,6 +68,7 @@ struct Tile {
   const uint8_t* big;
   int layer;
   const float* small;
+  uint64_t corr;        // MODE_H8: bit i = big layer i consumes the e4m3 correction (CORR_SLOT)
 };
 
 __device__ __forceinline__ bool in_range(int p, int L) { return p >= 0 && p < L; }
@@ -168,37 +171,55 @@ template <> struct Op<MODE_X3> {
   }
 };
 
-// plain bf16 on the same 256-byte rows (used by the CBAM segments): hi plane only, one MFMA.
-template <> struct Op<MODE_B1> {
+// plain bf16 (MODE_B1, 'bf16-unsafe') or f16 (MODE_F16, RDN_F16) on the same 256-byte rows (used by
+// the CBAM networks): hi plane only, one MFMA per product.
+typedef _Float16 h16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x4_t __attribute__((ext_vector_type(4)));
+template <typename E> struct S16Types;
+template <> struct S16Types<__bf16> {
+  typedef bf16x8 V8;
+  typedef bf16x4 V4;
+  __device__ static f32x4 mma(V8 a, V8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+};
+template <> struct S16Types<_Float16> {
+  typedef h16x8_t V8;
+  typedef h16x4_t V4;
+  __device__ static f32x4 mma(V8 a, V8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+};
+template <typename E> struct OpS16 {
+  typedef typename S16Types<E>::V8 V8;
+  typedef typename S16Types<E>::V4 V4;
   static constexpr int KSTEPS = 6;
-  struct A { bf16x8 hi; };
-  struct B { bf16x8 hi; };
+  struct A { V8 hi; };
+  struct B { V8 hi; };
   __device__ static A load_a(const uint8_t* layer, int m, int s, int lane) {
-    return A{((const bf16x8*)layer)[((m * 6 + s) * 2) * 64 + lane]};
+    return A{((const V8*)layer)[((m * 6 + s) * 2) * 64 + lane]};
   }
   __device__ static B load_b(const char* act, int prow, int s, int q) {
-    return B{*(const bf16x8*)(act + off_f32(prow, 64 * (s & 1) + 16 * q))};
+    return B{*(const V8*)(act + off_f32(prow, 64 * (s & 1) + 16 * q))};
   }
   __device__ static int tap(int s) { return s >> 1; }
   static constexpr int PLANES = 1;
   __device__ static int bslot(int s, int q, int) { return 4 * (s & 1) + q; }
   __device__ static int sbyte(int c0, int) { return 2 * c0; }
   __device__ static B load_b_at(const char* act, const uint32_t (&ad)[PLANES], uint32_t off) {
-    return B{*(const bf16x8*)(act + ad[0] + off)};
+    return B{*(const V8*)(act + ad[0] + off)};
   }
   __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v) {
-    *(bf16x4*)(act + ad[0] + off) = __builtin_convertvector(v, bf16x4);
+    *(V4*)(act + ad[0] + off) = __builtin_convertvector(v, V4);
   }
   __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc, uint32_t, int) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, acc, 0, 0, 0);
+    return S16Types<E>::mma(a.hi, b.hi, acc);
   }
   __device__ static void store4(char* act, int prow, int c0, f32x4 v) {
-    *(bf16x4*)(act + off_f32(prow, 2 * c0)) = __builtin_convertvector(v, bf16x4);
+    *(V4*)(act + off_f32(prow, 2 * c0)) = __builtin_convertvector(v, V4);
   }
   __device__ static f32x4 load4(const char* act, int prow, int c0) {
-    return __builtin_convertvector(*(const bf16x4*)(act + off_f32(prow, 2 * c0)), f32x4);
+    return __builtin_convertvector(*(const V4*)(act + off_f32(prow, 2 * c0)), f32x4);
   }
 };
+template <> struct Op<MODE_B1> : OpS16<__bf16> {};
+template <> struct Op<MODE_F16> : OpS16<_Float16> {};
 
 // f16 main product + block-scaled e4m3 correction (RDN_F16F8).  Row = [hi: 64 ch f16 (128 B) |
 // e4m3(hi / 4) (64 B) | e4m3(lo * 2^9) (64 B)], v = hi + lo, channels in h16_channel order within
@@ -285,6 +306,12 @@ template <> struct Op<MODE_H8> {
     const f16x8* f = (const f16x8*)layer + (m * 6 + 2 * s) * 64 + lane;
     return A{{f[0], f[64]}, *(const i32x8*)(layer + H8_CORR_OFF + ((m * 3 + s) * 64 + lane) * 32)};
   }
+  // the f16 fragments only (the next layer is uncorrected: its e4m3 fragments are never read)
+  __device__ static void load_a_main(const uint8_t* layer, int m, int s, int lane, A& a) {
+    const f16x8* f = (const f16x8*)layer + (m * 6 + 2 * s) * 64 + lane;
+    a.h[0] = f[0];
+    a.h[1] = f[64];
+  }
   __device__ static int tap(int s) { return s; }
   static constexpr int PLANES = 4;
   // B fragment of k-step s: f16 slots q (channels 0-31) and 4+q (32-63), e4m3 hi / lo bytes 16q..16q+15
@@ -295,9 +322,23 @@ template <> struct Op<MODE_H8> {
     return p == 0 ? 16 * slot + 8 * half : (p == 1 ? 128 : 192) + 8 * slot + 4 * half;
   }
   __device__ static B load_b_at(const char* act, const uint32_t (&ad)[PLANES], uint32_t off) {
+#if defined(RDN_ABLATE_H8_PLAIN)        // diagnostic (tools/ablate.py): f16 only, no correction traffic
+    return B{{*(const f16x8*)(act + ad[0] + off), *(const f16x8*)(act + ad[1] + off)}, i32x8{}};
+#endif
     const i32x4v ch = *(const i32x4v*)(act + ad[2] + off), cl = *(const i32x4v*)(act + ad[3] + off);
     return B{{*(const f16x8*)(act + ad[0] + off), *(const f16x8*)(act + ad[1] + off)},
              __builtin_shufflevector(ch, cl, 0, 1, 2, 3, 4, 5, 6, 7)};
+  }
+  // per-layer correction (RDN_F16MIX): without it only the f16 planes are read
+  __device__ static B load_b_at(const char* act, const uint32_t (&ad)[PLANES], uint32_t off, bool cin) {
+    B b;
+    b.h[0] = *(const f16x8*)(act + ad[0] + off);
+    b.h[1] = *(const f16x8*)(act + ad[1] + off);
+    if (cin) {
+      const i32x4v ch = *(const i32x4v*)(act + ad[2] + off), cl = *(const i32x4v*)(act + ad[3] + off);
+      b.c = __builtin_shufflevector(ch, cl, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    return b;
   }
   __device__ static B load_b(const char* act, int prow, int s, int q) {
     uint32_t ad[PLANES];
@@ -316,9 +357,16 @@ template <> struct Op<MODE_H8> {
   }
   __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc, uint32_t sa, int s) {
     const int sb = (__builtin_amdgcn_workitem_id_x() & 32) ? H8_LO_E8M0 : H8_HI_E8M0;   // lanes 32-63: the lo blocks
+#if !defined(RDN_ABLATE_H8_PLAIN)
     if (s == 0) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 0, (int)sa, 0, sb);
     else if (s == 1) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 1, (int)sa, 0, sb);
     else acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 2, (int)sa, 0, sb);
+#endif
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[0], b.h[0], acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[1], b.h[1], acc, 0, 0, 0);
+  }
+  __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc, uint32_t sa, int s, bool cin) {
+    if (cin) return mma(a, b, acc, sa, s);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[0], b.h[0], acc, 0, 0, 0);
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[1], b.h[1], acc, 0, 0, 0);
   }
@@ -494,9 +542,26 @@ __device__ __forceinline__ void two_sum(f32x4& hi, f32x4& c) {
 // Sequence: C0 | C1 | S0+C2 | S1+C3 | S2 S3 |.   id[16] = [block][N-tile][M-tile] identities.
 // EDGE = false: the tile holds no position outside [0, L) (interior tiles of a spectrum), so the
 // write-back skips the per-row zeroing.
-template <int MODE, int EPI, int S, bool EDGE = true, int NBK = 4>
+// MODE_H8 per-layer correction (RDN_F16F8: every layer; RDN_F16MIX: the layers of the blob's mask,
+// CORR_SLOT): cin = this layer reads the e4m3 planes and runs the correction MFMA, otherwise only
+// the f16 product (one MFMA per product); cout = its output is written with the e4m3 planes, which
+// the next layer needs if it is corrected, and every reader of load4 (head, identity re-add, CBAM)
+// needs: `out_full` marks such a last conv.  Both are wave-uniform (scalar branches).
+// MODE_H8 per-layer correction (RDN_F16F8: every layer; RDN_F16MIX: RRCDNet's calibrated tail):
+// CIN = this layer reads the e4m3 planes and runs the correction MFMA, otherwise only the f16
+// product (one MFMA per product); COUT = its output is written with the e4m3 planes, which the next
+// layer needs if it is corrected and every load4 reader (head, identity re-add, CBAM) needs; LOADC =
+// the next layer's e4m3 weight fragments are prefetched (only a corrected layer reads them).  All
+// three are template parameters: as wave-uniform runtime branches inside the k-step stream they cost
+// the all-corrected kernel 18 % and the uncorrected one 38 % (measured), and a per-layer runtime
+// dispatch between instantiations inside one loop made the compiler spill 1,400-8,000 VGPRs, so a
+// mixed network is written as straight runs of one instantiation each (fused_inplace.hip).
+template <int MODE, int EPI, int S, bool EDGE = true, int NBK = 4, bool CIN = true, bool COUT = true,
+          bool LOADC = true>
 __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4], LayerA<MODE>& a, bool has_next) {
   using O = Op<MODE>;
+  constexpr bool cin = MODE != MODE_H8 || CIN;
+  constexpr bool cout = MODE != MODE_H8 || COUT;
   using TG = TileGeo<NBK>;
   constexpr int NB = NBK, NT = IP_NT, MT = IP_MT, BR = IP_BR;
   constexpr int TS = O::KSTEPS / 3;                  // k-steps per tap
@@ -554,13 +619,17 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
       asm volatile("" : "+v"(badr2[s][p]));         // a register of its own, not re-derived per read
     }
 #endif
+  auto ldb = [&](const uint32_t (&ad)[O::PLANES], uint32_t off) -> typename O::B {
+    if constexpr (MODE == MODE_H8) return O::load_b_at(tl.lds, ad, off, cin);
+    else return O::load_b_at(tl.lds, ad, off);
+  };
   auto read_b = [&](int j, int s, int i) -> typename O::B {
-    if (TG::WRAP && j == 0 && s < TS && i == 0) return O::load_b_at(tl.lds, bfirst[s], 0);
-    if (TG::WRAP && j == NB - 1 && s >= 2 * TS && i == NT - 1) return O::load_b_at(tl.lds, blast[s - 2 * TS], 0);
+    if (TG::WRAP && j == 0 && s < TS && i == 0) return ldb(bfirst[s], 0);
+    if (TG::WRAP && j == NB - 1 && s >= 2 * TS && i == NT - 1) return ldb(blast[s - 2 * TS], 0);
 #if RDN_IP_HIBASE
-    if (j >= 2) return O::load_b_at(tl.lds, badr2[s], (uint32_t)(BR * (j - 2) + 16 * i) * ROWB_F32);
+    if (j >= 2) return ldb(badr2[s], (uint32_t)(BR * (j - 2) + 16 * i) * ROWB_F32);
 #endif
-    return O::load_b_at(tl.lds, badr[s], (uint32_t)(BR * j + 16 * i) * ROWB_F32);
+    return ldb(badr[s], (uint32_t)(BR * j + 16 * i) * ROWB_F32);
   };
 #pragma unroll
   for (int mm = 0; mm < MT; ++mm)
@@ -594,6 +663,21 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
     const int rb = BR * j + (BR / 4) * nq;
     const bool inside = !EDGE || (tl.base + rb >= 0 && tl.base + rb + BR / 4 <= tl.L);
     const bool zero = !inside && !in_range(tl.base + rb + 16 * i + c16, tl.L);
+    if (!cout) {                 // plain f16 output (the next layer is uncorrected): no e4m3 planes
+      f16x4 hv[MT];
+#pragma unroll
+      for (int mm = 0; mm < MT; ++mm) {
+        f32x4 v = res[j][i][mm];
+        if (EPI & ADD_ID) v += id[(j * NT + i) * MT + mm];
+        if (EPI & RELU) v = __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
+        if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
+        hv[mm] = __builtin_convertvector(v, f16x4);
+      }
+      *(f16x8*)(tl.lds + sadr[0][0] + (uint32_t)(BR * j + 16 * i) * ROWB_F32) =
+          __builtin_shufflevector(hv[0], hv[1], 0, 1, 2, 3, 4, 5, 6, 7);
+      return;
+    }
     H8Split x[MT];
 #pragma unroll
     for (int mm = 0; mm < MT; ++mm) {
@@ -608,6 +692,12 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #if defined(RDN_ABLATE_NOSTORE)
     if (x[0].hi8 == 0x12345678u)
+#endif
+#if defined(RDN_ABLATE_H8_PLAIN)
+    {
+      *(f16x8*)(tl.lds + sadr[0][0] + off) = __builtin_shufflevector(x[0].hi, x[1].hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    if (false)
 #endif
     {
       *(f16x8*)(tl.lds + sadr[0][0] + off) = __builtin_shufflevector(x[0].hi, x[1].hi, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -664,7 +754,10 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
 #pragma unroll
-        for (int mm = 0; mm < MT; ++mm) part[s % SP][i][mm] = O::mma(a[mm][s], bnext[i], part[s % SP][i][mm], sc_l[mm], s);
+        for (int mm = 0; mm < MT; ++mm) {
+          if constexpr (MODE == MODE_H8) part[s % SP][i][mm] = O::mma(a[mm][s], bnext[i], part[s % SP][i][mm], sc_l[mm], s, cin);
+          else part[s % SP][i][mm] = O::mma(a[mm][s], bnext[i], part[s % SP][i][mm], sc_l[mm], s);
+        }
         if (s + 1 < O::KSTEPS) bnext[i] = read_b(j, s + 1, i);
         else if (j + 1 < NB) bnext[i] = read_b(j + 1, 0, i);
         if constexpr (COMP) {
@@ -688,7 +781,10 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
       }
       if (j == NB - 1 && has_next) {                                   // last use of a[.][s]
 #pragma unroll
-        for (int mm = 0; mm < MT; ++mm) a[mm][s] = O::load_a(wnext, MT * mp + mm, s, lane);
+        for (int mm = 0; mm < MT; ++mm) {
+          if constexpr (MODE == MODE_H8 && !LOADC) O::load_a_main(wnext, MT * mp + mm, s, lane, a[mm][s]);
+          else a[mm][s] = O::load_a(wnext, MT * mp + mm, s, lane);
+        }
       }
       if (j >= 2) {
         constexpr int NP = NT * MT;
@@ -796,6 +892,13 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 template <int MODE, bool RES> struct Geo { static constexpr int S = 1; };
 template <> struct Geo<MODE_F32, false> { static constexpr int S = RDN_F32_COMP ? 0 : 2; };
 
+// the blob's per-layer correction mask (common.hpp CORR_SLOT), a scalar load
+__device__ __forceinline__ uint64_t corr_mask(const uint8_t* blob) {
+  const cfloat* p = (const cfloat*)(blob + CORR_SLOT * SMALL_SLOT_FLOATS * 4);
+  const uint32_t lo = __float_as_uint(p[0]), hi = __float_as_uint(p[1]);
+  return (uint64_t)hi << 32 | lo;
+}
+
 __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const float* x, int L, int T,
                                           int tiles, int halo, int& n_out) {
   const int n = __builtin_amdgcn_workgroup_id_x() / tiles, tile = __builtin_amdgcn_workgroup_id_x() - n * tiles;
@@ -808,6 +911,7 @@ __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const 
   tl.small = (const float*)blob;
   tl.big = blob + SMALL_BYTES;
   tl.layer = 0;
+  tl.corr = corr_mask(blob);
   return tl;
 }
 

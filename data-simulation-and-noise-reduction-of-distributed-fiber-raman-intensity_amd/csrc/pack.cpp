@@ -16,6 +16,9 @@
 namespace rdn {
 
 static constexpr double BN_EPS = 1e-5;
+uint64_t f16mix_default_mask(int arch);
+void set_corr_mask(void* blob, uint64_t mask);
+
 
 std::vector<Op> net_spec(int arch) {
   std::vector<Op> s;
@@ -129,14 +132,19 @@ static bool has_cbam(const std::vector<Op>& spec) {
     if (o.kind == OpKind::CBAM) return true;
   return false;
 }
+// layouts: F32, F16F8, BF16 / F16 (fused16.hip, head as an MFMA layer), BF16X3 (also the in-place
+// plain-bf16 mode of the CBAM networks), F16X = F16 on the CBAM networks (split-bf16 geometry, f16 hi)
+constexpr int F16X = 100;
 int big_layout(const std::vector<Op>& spec, int dtype) {
   if (dtype == F32) return F32;
-  if (dtype == F16F8) return F16F8;
+  if (dtype == F16F8 || dtype == F16MIX) return F16F8;
   if (dtype == BF16 && !has_cbam(spec)) return BF16;
+  if (dtype == F16) return has_cbam(spec) ? F16X : F16;
   return BF16X3;
 }
 int big_layers(const std::vector<Op>& spec, int dtype) {
-  const bool head_big = big_layout(spec, dtype) == BF16;
+  const int lay = big_layout(spec, dtype);
+  const bool head_big = lay == BF16 || lay == F16;
   int n = 0;
   for (const Op& o : spec) n += o.kind == OpKind::BIG || (o.kind == OpKind::HEAD && head_big);
   return n;
@@ -197,7 +205,27 @@ static uint16_t to_bf16(double v) {      // fp64 -> fp32 -> bf16, round to neare
   return (uint16_t)(u >> 16);
 }
 
-static void pack_big_bf16(const Folded& f, uint8_t* dst) {
+static uint16_t to_f16(double v) {       // fp64 -> fp32 -> f16, round to nearest even
+  const _Float16 h = (_Float16)(float)v;
+  uint16_t u;
+  std::memcpy(&u, &h, 2);
+  return u;
+}
+
+static double from16(uint16_t u, bool f16) {
+  if (f16) {
+    _Float16 h;
+    std::memcpy(&h, &u, 2);
+    return (double)(float)h;
+  }
+  const uint32_t b = (uint32_t)u << 16;
+  float f;
+  std::memcpy(&f, &b, 4);
+  return (double)f;
+}
+
+// fused16.hip layout; f16: the RDN_F16 instantiation (same fragments, f16 bits)
+static void pack_big_bf16(const Folded& f, uint8_t* dst, bool f16 = false) {
   uint16_t* frag = (uint16_t*)dst;
   for (int m = 0; m < 4; ++m)
     for (int s = 0; s < 6; ++s)
@@ -205,8 +233,13 @@ static void pack_big_bf16(const Folded& f, uint8_t* dst) {
         for (int j = 0; j < 8; ++j) {
           const int t = s >> 1, u = s & 1;
           const int co = 16 * m + (lane & 15), ci = h16_channel(4 * u + (lane >> 4), j);
-          const double v = co < f.cout ? f.W(co, ci, t) : 0.0;
-          frag[(((m * 6 + s) * 64) + lane) * 8 + j] = to_bf16(v);
+          double v = co < f.cout ? f.W(co, ci, t) : 0.0;
+          // a head (cout = 1): row 1 carries the residue of row 0's rounding (fused16.hip head)
+          if (f.cout == 1 && co == 1) {
+            const double w = f.W(0, ci, t);
+            v = w - from16(f16 ? to_f16(w) : to_bf16(w), f16);
+          }
+          frag[(((m * 6 + s) * 64) + lane) * 8 + j] = f16 ? to_f16(v) : to_bf16(v);
         }
   float* bias = (float*)(dst + BIG_FRAG_BYTES_BF16);
   for (int c = 0; c < C; ++c) bias[c] = c < f.cout ? (float)f.b[c] : 0.f;
@@ -226,7 +259,9 @@ static void pack_big_f32(const Folded& f, uint8_t* dst) {
   for (int c = 0; c < C; ++c) bias[c] = (float)f.b[c];
 }
 
-static void pack_big_x3(const Folded& f, uint8_t* dst) {
+// split-bf16 layout; f16: the in-place single-plane f16 mode of the CBAM networks (RDN_F16 there),
+// which reads only the hi fragments, here f16(W)
+static void pack_big_x3(const Folded& f, uint8_t* dst, bool f16 = false) {
   uint16_t* frag = (uint16_t*)dst;
   for (int m = 0; m < 4; ++m)
     for (int s = 0; s < 6; ++s)
@@ -235,6 +270,11 @@ static void pack_big_x3(const Folded& f, uint8_t* dst) {
           const int t = s >> 1, u = s & 1;
           const int co = 16 * m + (lane & 15), ci = 32 * u + 8 * (lane >> 4) + j;
           const float w = (float)f.W(co, ci, t);
+          if (f16) {
+            frag[((((m * 6 + s) * 2 + 0) * 64) + lane) * 8 + j] = to_f16(w);
+            frag[((((m * 6 + s) * 2 + 1) * 64) + lane) * 8 + j] = 0;
+            continue;
+          }
           const uint16_t hi = to_bf16(w);
           const uint32_t hib = (uint32_t)hi << 16;
           float hf;
@@ -380,7 +420,7 @@ static bool pack_cbam(Reader& rd, const Op& o, float* small) {
 }
 
 static size_t layer_bytes(int layout) {
-  return layout == BF16 ? BIG_BYTES_BF16 : layout == F16F8 ? BIG_BYTES_H8 : BIG_BYTES_F32;
+  return layout == BF16 || layout == F16 ? BIG_BYTES_BF16 : layout == F16F8 ? BIG_BYTES_H8 : BIG_BYTES_F32;
 }
 
 size_t packed_bytes(const std::vector<Op>& spec, int dtype) {
@@ -393,7 +433,10 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
                  size_t cap) {
   const std::vector<Op> spec = net_spec(arch);
   if (spec.empty()) return "unknown arch " + std::to_string(arch);
-  if (dtype != F32 && dtype != BF16 && dtype != BF16X3 && dtype != F16F8) return "unknown dtype " + std::to_string(dtype);
+  if (dtype != F32 && dtype != BF16 && dtype != BF16X3 && dtype != F16F8 && dtype != F16 && dtype != F16MIX)
+    return "unknown dtype " + std::to_string(dtype);
+  if (dtype == F16MIX && arch != RRCDNET)
+    return "unsupported: RDN_F16MIX is built for RRCDNet (the other networks meet 2e-2 in plain RDN_F16)";
   const size_t need = packed_bytes(spec, dtype);
   if (cap < need) return "destination too small: need " + std::to_string(need) + " bytes";
   uint8_t* out = (uint8_t*)dst;
@@ -413,8 +456,8 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
         break;
       case OpKind::BIG:
         if (!fold(rd, o, C, C, f)) return rd.err;
-        if (layout == BF16) pack_big_bf16(f, big + layer * big_bytes);
-        else if (layout == BF16X3) pack_big_x3(f, big + layer * big_bytes);
+        if (layout == BF16 || layout == F16) pack_big_bf16(f, big + layer * big_bytes, layout == F16);
+        else if (layout == BF16X3 || layout == F16X) pack_big_x3(f, big + layer * big_bytes, layout == F16X);
         else if (layout == F16F8) pack_big_h8(f, big + layer * big_bytes);
         else pack_big_f32(f, big + layer * big_bytes);
         ++layer;
@@ -422,7 +465,7 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
       case OpKind::HEAD:
         if (!fold(rd, o, C, 1, f)) return rd.err;
         pack_small_conv(f, small + o.slot * SMALL_SLOT_FLOATS);
-        if (layout == BF16) pack_big_bf16(f, big + (layer++) * big_bytes);
+        if (layout == BF16 || layout == F16) pack_big_bf16(f, big + (layer++) * big_bytes, layout == F16);
         break;
       case OpKind::CBAM:
         if (!pack_cbam(rd, o, small)) return rd.err;
@@ -430,7 +473,27 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
     }
   }
   if (rd.i != n) return "too many tensors: consumed " + std::to_string(rd.i) + " of " + std::to_string(n);
+  if (dtype == F16F8 || dtype == F16MIX) set_corr_mask(out, dtype == F16F8 ? ~0ull : f16mix_default_mask(arch));
   return "";
+}
+
+// RDN_F16MIX: the big layers (execution order) that keep the e4m3 correction.  Plain f16 (RDN_F16)
+// meets the 2e-2 bar on every golden fixture except trained RRCDNet (3.5e-2 fused / 2.6e-2 with the
+// exact head input of the in-place path); the head's cancellation x - (r + l)/2 amplifies the
+// rounding of the right branch's last layers most (tools/f16mix_select.py, greedy on the GPU), and
+// correcting right_net.15-17 (big layers 12-14) brings it to 1.36e-2 (tools/f16mix_masks.py).  The
+// pattern is compiled into the kernel (fused_inplace.hip RRCDNET_F16MIX_TAIL); the blob records it.
+uint64_t f16mix_default_mask(int arch) {
+  return arch == RRCDNET ? (0x7ull << 12) : 0;
+}
+void set_corr_mask(void* blob, uint64_t mask) {
+  uint32_t* w = (uint32_t*)((uint8_t*)blob + (size_t)CORR_SLOT * SMALL_SLOT_FLOATS * 4);
+  w[0] = (uint32_t)mask;
+  w[1] = (uint32_t)(mask >> 32);
+}
+uint64_t get_corr_mask(const void* blob) {
+  const uint32_t* w = (const uint32_t*)((const uint8_t*)blob + (size_t)CORR_SLOT * SMALL_SLOT_FLOATS * 4);
+  return (uint64_t)w[1] << 32 | w[0];
 }
 
 }  // namespace rdn

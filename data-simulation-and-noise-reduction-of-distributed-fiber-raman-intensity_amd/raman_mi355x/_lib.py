@@ -47,6 +47,9 @@ class GenParams(ctypes.Structure):
 _SIGNATURES = {
     "rdn_version": ([], ctypes.c_int),
     "rdn_build_id": ([], ctypes.c_char_p),
+    "rdn_default_correction_mask": ([ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+    "rdn_get_correction_mask": ([ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                 ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "rdn_forward_status": ([ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                             ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
     "rdn_last_error": ([], ctypes.c_char_p),

@@ -12,14 +12,42 @@ from . import _lib
 
 ARCHS = ("DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN")
 ARCH_ID = {a: i for i, a in enumerate(ARCHS)}
+CBAM_ARCHS = ("ADSDN", "APIDN")
 # Engine arithmetic modes (include/raman_mi355x.h rdn_dtype).  Every name here except
 # "bf16-unsafe" meets its north-star tolerance on every golden fixture (fp32: 1e-5 max-relative;
 # 16-bit modes: 2e-2 max-abs).  Single-rounding bf16 does NOT (0.24 on trained RRCDNet),
 # so it is reachable only under that explicit name; plain "bf16" / torch.bfloat16 is refused with a
 # pointer to the tolerance-meeting 16-bit modes instead of silently returning out-of-contract results.
-DTYPE_ID = {"fp32": 0, "float32": 0, "bf16-unsafe": 1, "bf16_unsafe": 1, "bf16x3": 2, "f16f8": 3}
-DTYPE_NAME = {0: "fp32", 1: "bf16-unsafe", 2: "bf16x3", 3: "f16f8"}
-SAFE_16BIT = ("f16f8", "bf16x3")
+DTYPE_ID = {"fp32": 0, "float32": 0, "bf16-unsafe": 1, "bf16_unsafe": 1, "bf16x3": 2, "f16f8": 3, "f16": 4,
+            "float16": 4, "f16-plain": 4, "f16mix": 5}
+DTYPE_NAME = {0: "fp32", 1: "bf16-unsafe", 2: "bf16x3", 3: "f16f8", 4: "f16", 5: "f16mix"}
+SAFE_16BIT = ("f16", "f16f8", "bf16x3")
+F16, F16MIX = 4, 5
+
+
+def default_correction_mask(arch):
+    """The layers RDN_F16MIX corrects for ``arch`` (0: plain f16 already meets the 2e-2 bar there)."""
+    m = ctypes.c_uint64()
+    _lib.check(_lib.lib().rdn_default_correction_mask(_arch(arch), ctypes.byref(m)), "rdn_default_correction_mask")
+    return m.value
+
+
+def correction_mask(arch, dtype, host_blob):
+    """Correction mask recorded in a packed (host) blob."""
+    m = ctypes.c_uint64()
+    _lib.check(_lib.lib().rdn_get_correction_mask(_arch(arch), _dtype(dtype), ctypes.c_void_p(host_blob.data_ptr()),
+                                                  host_blob.numel(), ctypes.byref(m)), "rdn_get_correction_mask")
+    return m.value
+
+
+def resolve_dtype(arch, dtype):
+    """ABI dtype code for a user dtype.  'f16' is the fastest arithmetic within the 2e-2 bar: plain f16
+    (RDN_F16) where that suffices, f16 with the compiled-in e4m3-corrected layers (RDN_F16MIX) where it
+    does not (RRCDNet).  'f16-plain' forces RDN_F16 everywhere."""
+    code = _dtype(dtype)
+    if dtype == "f16" and default_correction_mask(arch):
+        code = F16MIX
+    return code
 
 
 def _arch(arch):
@@ -35,15 +63,15 @@ def _dtype(dtype):
     if isinstance(dtype, int) and dtype in DTYPE_NAME:
         return dtype
     if isinstance(dtype, torch.dtype):
-        dtype = {torch.float32: "fp32", torch.bfloat16: "bf16"}.get(dtype, str(dtype))
+        dtype = {torch.float32: "fp32", torch.bfloat16: "bf16", torch.float16: "f16"}.get(dtype, str(dtype))
     if dtype in ("bf16", "bfloat16"):
         raise ValueError("engine dtype 'bf16' (one bf16 rounding per operand) does not meet the 2e-2 bf16 "
-                         "tolerance on trained weights (0.24 on trained RRCDNet); use 'f16f8' or 'bf16x3' "
+                         "tolerance on trained weights (0.24 on trained RRCDNet); use 'f16', 'f16f8' or 'bf16x3' "
                          f"({', '.join(SAFE_16BIT)}: within 2e-2), or opt in explicitly with 'bf16-unsafe'")
     try:
         return DTYPE_ID[dtype]
     except KeyError:
-        raise ValueError(f"unknown engine dtype {dtype!r}; expected one of 'fp32', 'f16f8', 'bf16x3', "
+        raise ValueError(f"unknown engine dtype {dtype!r}; expected one of 'fp32', 'f16', 'f16f8', 'bf16x3', "
                          "'bf16-unsafe'") from None
 
 
@@ -103,9 +131,6 @@ def _check_out(t, name, shape, device, dtype=torch.float32):
         raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
     if not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
-
-
-CBAM_ARCHS = ("ADSDN", "APIDN")
 
 
 def forward(arch, dtype, packed, x, out=None, check=True):

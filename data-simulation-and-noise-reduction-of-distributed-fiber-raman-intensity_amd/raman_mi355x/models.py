@@ -36,6 +36,7 @@ class _EngineNet(nn.Module):
     def __init__(self):
         super().__init__()
         self._engine_dtype = "fp32"
+        self._engine_code = 0
         self._packed = None
         self._packed_key = None
         self._tensor_cache = None
@@ -45,16 +46,26 @@ class _EngineNet(nn.Module):
     def engine_dtype(self):
         return self._engine_dtype
 
+    @property
+    def engine_code(self):
+        """The C-ABI dtype (rdn_dtype) the forward runs: 'f16' resolves per network (engine.resolve_dtype)."""
+        return self._engine_code
+
     def set_engine_dtype(self, dtype):
         """Arithmetic of the 64->64 convolutions:
         'fp32'        exact-fp32 MFMA with compensated accumulation: within 1e-5 of the fp32 reference;
+        'f16'         one f16 MFMA per product, f16 activations, fp32 accumulation: the fastest mode
+                      within 2e-2.  On RRCDNet, where plain f16 misses the bar, the last three
+                      right-branch layers keep the e4m3 correction (RDN_F16MIX, 1.4e-2);
+        'f16-plain'   plain f16 on every layer (RDN_F16) -- misses 2e-2 on trained RRCDNet (3.5e-2);
         'f16f8'       f16 product + one block-scaled e4m3 MFMA carrying both correction terms (~15
                       significant bits): within 2e-2 (measured <= 1e-3);
         'bf16x3'      split bf16, three bf16 MFMAs per product: within 2e-2 (measured <= 6e-4);
         'bf16-unsafe' one bf16 rounding per operand: fastest, NO tolerance guarantee (0.24 on trained
                       RRCDNet).  Plain 'bf16' is refused (engine._dtype)."""
-        code = engine._dtype(dtype)
-        self._engine_dtype = engine.DTYPE_NAME[code]
+        code = engine.resolve_dtype(self.ARCH, dtype)
+        self._engine_dtype = dtype if isinstance(dtype, str) and dtype in engine.DTYPE_ID else engine.DTYPE_NAME[code]
+        self._engine_code = code
         return self
 
     # -- packing -----------------------------------------------------------------------------
@@ -76,14 +87,14 @@ class _EngineNet(nn.Module):
     def _state_key(self, device):
         # identity + storage + version counter of each tensor: in-place updates (optimizer steps,
         # .add_(), load_state_dict's copy_) bump _version; replacements change identity or storage
-        return (str(device), self._engine_dtype,
+        return (str(device), self._engine_code,
                 tuple((t.data_ptr(), t._version) for _, _, t in self._slots()), len(self._tensor_cache))
 
     def packed_weights(self, device):
         key = self._state_key(device)
         if key != self._packed_key:
             with torch.no_grad():
-                self._packed = engine.pack(self.ARCH, self.state_dict(), self._engine_dtype, device)
+                self._packed = engine.pack(self.ARCH, self.state_dict(), self._engine_code, device)
             self._packed_key = key
         return self._packed
 
@@ -101,7 +112,7 @@ class _EngineNet(nn.Module):
             raise ValueError(f"{type(self).__name__}: expected input (N, 1, L), got {tuple(x.shape)}")
         if x.dtype != torch.float32:
             raise TypeError(f"{type(self).__name__}: expected float32 input, got {x.dtype}")
-        return engine.forward(self.ARCH, self._engine_dtype, self.packed_weights(x.device), x)
+        return engine.forward(self.ARCH, self._engine_code, self.packed_weights(x.device), x)
 
 
 def _check_defaults(name, in_channels, num_res_blocks):

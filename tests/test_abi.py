@@ -248,3 +248,17 @@ def test_host_sanitizer_pack(arch, dtype, tmp_path):
     assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr
     blob = np.fromfile(tmp_path / "blob.bin", dtype=np.uint8)
     np.testing.assert_array_equal(blob, engine.pack(arch, sd, dtype, "cpu").numpy())
+
+
+def test_correction_masks_recorded_in_blob():
+    """RDN_F16F8 blobs record every layer as corrected, RDN_F16MIX (RRCDNet only) the compiled-in tail
+    right_net.15-17 = big layers 12-14; the other networks refuse RDN_F16MIX."""
+    from raman_mi355x import engine, _lib
+    sd = golden_state_dict("RRCDNet", "trained")
+    assert engine.correction_mask("RRCDNet", "f16f8", engine.pack("RRCDNet", sd, "f16f8", "cpu")) == (1 << 64) - 1
+    assert engine.correction_mask("RRCDNet", "f16mix", engine.pack("RRCDNet", sd, "f16mix", "cpu")) == 0x7 << 12
+    assert engine.default_correction_mask("RRCDNet") == 0x7 << 12
+    for arch in ("DenoiseCNN", "DSDN", "PIDN", "ADSDN", "APIDN"):
+        assert engine.default_correction_mask(arch) == 0
+        with pytest.raises(_lib.EngineError, match="RRCDNet"):
+            engine.pack(arch, golden_state_dict(arch, "synth"), "f16mix", "cpu")
