@@ -31,13 +31,22 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "denoised spectra/sec (node) RRCDNet bf16/fp32 at 1/2/4/8 GPU; % MFMA peak"
 # Dense MFMA peaks, MI355X_MICROARCH.md §Chip-level parameters (spec values)
-PEAK_TFLOPS = {"f16": 2500.0, "bf16-unsafe": 2500.0, "bf16x3": 2500.0, "f16f8": 2500.0, "fp32": 157.3}
+PEAK_TFLOPS = {"f16": 2500.0, "f16-plain": 2500.0, "bf16-unsafe": 2500.0, "bf16x3": 2500.0, "f16f8": 2500.0, "fp32": 157.3}
 # conv layer counts per network: (64->64 convs, stems, heads) — SURVEY.md §2 table
 LAYERS = {"DenoiseCNN": (18, 1, 1), "RRCDNet": (29, 2, 2), "DSDN": (32, 1, 1), "PIDN": (30, 1, 1),
           "ADSDN": (32, 1, 1), "APIDN": (30, 1, 1)}
 SA_CONVS = {"ADSDN": 17, "APIDN": 15}
 # MFMA cycles per product relative to one bf16 MFMA (v_mfma_f32_16x16x32_bf16 = 16 cycles per K=32)
-MFMA_COST = {"f16": 1, "bf16-unsafe": 1, "bf16x3": 3, "f16f8": 2}
+# ('f16' on RRCDNet = RDN_F16MIX: 26 plain layers + 3 corrected at 2 units, bench.mfma_cost)
+MFMA_COST = {"f16": 1, "f16-plain": 1, "bf16-unsafe": 1, "bf16x3": 3, "f16f8": 2}
+
+
+def mfma_cost(arch, dtype):
+    """bf16-MFMA units executed per algorithmic product: RDN_F16MIX (Python 'f16' on RRCDNet) runs 3 of
+    its 29 big layers with the e4m3 correction (2 units) and the rest plain (1)."""
+    if dtype == "f16" and arch == "RRCDNet":
+        return (26 + 3 * 2) / 29
+    return MFMA_COST.get(dtype)
 
 
 def flops_per_spectrum(arch, L):
@@ -140,7 +149,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--arch", default="RRCDNet")
-    ap.add_argument("--dtype", default="f16", choices=["f16", "bf16-unsafe", "bf16x3", "f16f8", "fp32"])
+    ap.add_argument("--dtype", default="f16", choices=["f16", "f16-plain", "bf16-unsafe", "bf16x3", "f16f8", "fp32"])
     ap.add_argument("--batch", type=int, default=8192, help="spectra per GPU per step")
     ap.add_argument("--L", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=20250410)
@@ -210,7 +219,7 @@ def main():
 
     variants = {}
     if not args.no_variants:
-        for dt in ("f16", "f16f8", "bf16x3", "bf16-unsafe", "fp32"):
+        for dt in ("f16", "f16-plain", "f16f8", "bf16x3", "bf16-unsafe", "fp32"):
             if dt == args.dtype:
                 continue
             nb = B if dt != "fp32" else max(1, B // 4)
@@ -237,15 +246,16 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (on-device simulator, 数据集产生.py contract; random-init weights)",
             "config": {"workload": f"{args.arch} {args.dtype} fused forward, on-device simulator inputs "
-                                   "(BASELINE.json configs[2])",
+                                   "(BASELINE.json configs[2])", "engine_dtype_code": code,
                        "arch": args.arch, "signal_length": L, "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": tps * B if tps else None,
                          "traffic_source": tsrc, "algorithmic_bytes": 8 * L * B,
                          "kernel_ms": kernel_ms, "flops_per_launch": fl,
-                         "mfma_cost_per_product_bf16_units": MFMA_COST.get(args.dtype),
-                         "executed_bf16_equiv_tflops": achieved * MFMA_COST[args.dtype] if args.dtype in MFMA_COST else None},
+                         "mfma_cost_per_product_bf16_units": mfma_cost(args.arch, args.dtype),
+                         "executed_bf16_equiv_tflops": (achieved * mfma_cost(args.arch, args.dtype)
+                                                        if mfma_cost(args.arch, args.dtype) else None)},
             "variants": variants,
             "pipeline": pipeline,
             "metrics_mean": {k: sums[i] / sums[4] for i, k in enumerate(["MSE", "SSIM", "Smoothness", "Peak2Peak"])},

@@ -256,15 +256,15 @@ __global__ __launch_bounds__(THREADS) void segment(const uint8_t* __restrict__ b
     stem<MODE, true>(tl, 0);
     __syncthreads();
   }
-  double d[HEAD_ROWS];
+  double d[HeadOut<MODE>::ROWS];
   head<MODE>(tl, sg.head_slot, d);
-  float v[HEAD_ROWS];
+  float v[HeadOut<MODE>::ROWS];
   round_rows(d, v);
   if (sg.head_sigmoid) {
 #pragma unroll
-    for (int k = 0; k < HEAD_ROWS; ++k) v[k] = sigm(v[k]);
+    for (int k = 0; k < HeadOut<MODE>::ROWS; ++k) v[k] = sigm(v[k]);
   }
-  store_out(tl, y, n, v, sg.halo, T);
+  store_out<MODE>(tl, y, n, v, sg.halo, T);
 }
 
 
@@ -801,21 +801,21 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
       stem<MODE, true>(tl, 0);       // + h, recomputed from x
       __syncthreads();
     }
-    double d[HEAD_ROWS];
+    double d[HeadOut<MODE>::ROWS];
     head<MODE>(tl, 1, d);
-    float v[HEAD_ROWS];
+    float v[HeadOut<MODE>::ROWS];
     round_rows(d, v);
     if (!ADS) {
 #pragma unroll
-      for (int k = 0; k < HEAD_ROWS; ++k) v[k] = sigm(v[k]);
+      for (int k = 0; k < HeadOut<MODE>::ROWS; ++k) v[k] = sigm(v[k]);
     }
     // a timed-out hand-off anywhere in the grid: this spectrum's CBAM statistics may be incomplete,
     // so its outputs are NaN rather than plausible-looking garbage
     if (__hip_atomic_load(ta.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
 #pragma unroll
-      for (int k = 0; k < HEAD_ROWS; ++k) v[k] = __uint_as_float(0x7fc00000u);   // quiet NaN (bit pattern: -fno-honor-nans build)
+      for (int k = 0; k < HeadOut<MODE>::ROWS; ++k) v[k] = __uint_as_float(0x7fc00000u);   // quiet NaN (bit pattern: -fno-honor-nans build)
     }
-    store_out(tl, y, (int)n, v, ta.halo, ta.T);
+    store_out<MODE>(tl, y, (int)n, v, ta.halo, ta.T);
     __syncthreads();                 // the next spectrum's stem overwrites the rows the head read
     stamp(6);
   }

@@ -18,6 +18,7 @@ namespace ip {
 // 128-row blocks per tile: 640-row tiles (the whole LDS, no guard rows) everywhere except DSDN,
 // whose ResidualBlock identity lives in VGPRs (20 vs 16 f32x4 per lane at 640 rows: spills).
 template <int ARCH> struct NetGeo { static constexpr int NBK = 5; };
+
 #ifndef RDN_DSDN_NBK
 #define RDN_DSDN_NBK 4
 #endif
@@ -33,11 +34,11 @@ IP_BODY(denoisecnn) {
   stem<MODE, false, NBK>(tl, 0);
   __syncthreads();
   for (int i = 0; i < 18; ++i) conv<MODE, RELU, G::S, EDGE, NBK>(tl, 1, id, a, i + 1 < 18);
-  double d[HEAD_ROWS];
+  double d[HeadOut<MODE, NBK>::ROWS];
   head<MODE, NBK>(tl, 1, d);
-  float o[HEAD_ROWS];
+  float o[HeadOut<MODE, NBK>::ROWS];
   round_rows(d, o);
-  store_out(tl, y, n, o, H, T);
+  store_out<MODE, NBK>(tl, y, n, o, H, T);
 }
 
 IP_BODY(rrcdnet) {
@@ -52,14 +53,17 @@ IP_BODY(rrcdnet) {
   if constexpr (TAIL == 0) {
     for (int i = 0; i < 15; ++i) conv<MODE, RELU, G::S, EDGE, NBK>(tl, 1, id, a, true);
   } else {
-    // RDN_F16MIX: plain f16 layers, the last one writing the e4m3 planes, then TAIL corrected layers
-    // (right_net.15-17 for TAIL = 3: the layers whose f16 rounding the head's cancellation
-    // x - (r + l)/2 amplifies most, tools/f16mix_select.py)
+    // RDN_F16MIX: plain f16 layers (the correction compiled out), the last of them also writing the
+    // e4m3 planes, then TAIL corrected layers (right_net.15-17 for TAIL = 3: the layers whose f16
+    // rounding the head's cancellation x - (r + l)/2 amplifies most, tools/f16mix_select.py).
+    // (A wave split with all four M-tiles per wave -- half the LDS reads, twice the per-wave weight
+    // fragments -- measured 10 % slower: the layer is not LDS-bound, the extra L1 weight traffic is.)
     for (int i = 0; i < 14 - TAIL; ++i) conv<MODE, RELU, G::S, EDGE, NBK, false, false, false>(tl, 1, id, a, true);
     conv<MODE, RELU, G::S, EDGE, NBK, false, true, true>(tl, 1, id, a, true);
-    for (int i = 0; i < TAIL; ++i) conv<MODE, RELU, G::S, EDGE, NBK, true, true, true>(tl, 1, id, a, true);
+    for (int i = 0; i < TAIL; ++i) conv<MODE, RELU, G::S, EDGE, NBK, true, true, true>(tl, 1, id, a, i + 1 < TAIL);
+    load_layer_a<MODE>(tl, tl.layer, a);                // the left branch's first layer (f16 + e4m3)
   }
-  double r[HEAD_ROWS];
+  double r[HeadOut<MODE, NBK>::ROWS];
   head<MODE, NBK>(tl, 2, r);
   __syncthreads();               // the left stem overwrites the rows the right head just read
   stem<MODE, false, NBK>(tl, 1);
@@ -71,16 +75,16 @@ IP_BODY(rrcdnet) {
     for (int i = 0; i < 13; ++i) conv<MODE, RELU, G::S, EDGE, NBK, false, false, false>(tl, i == 7 ? 1 : 2, id, a, true);
     conv<MODE, RELU, G::S, EDGE, NBK, false, true, false>(tl, 2, id, a, false);
   }
-  double l[HEAD_ROWS];
+  double l[HeadOut<MODE, NBK>::ROWS];
   head<MODE, NBK>(tl, 3, l);
-  float o[HEAD_ROWS];
+  float o[HeadOut<MODE, NBK>::ROWS];
 #pragma unroll
-  for (int k = 0; k < HEAD_ROWS; ++k) {      // x - (r + l)/2 from the unrounded heads, one rounding
-    const int p = tl.base + (int)__builtin_amdgcn_workitem_id_x() + THREADS * k;
+  for (int k = 0; k < HeadOut<MODE, NBK>::ROWS; ++k) {      // x - (r + l)/2 from the unrounded heads, one rounding
+    const int p = tl.base + HeadOut<MODE, NBK>::row(k);
     const float xv = in_range(p, L) ? tl.x[p] : 0.f;
     o[k] = (float)((double)xv - (r[k] + l[k]) * 0.5);
   }
-  store_out(tl, y, n, o, H, T);
+  store_out<MODE, NBK>(tl, y, n, o, H, T);
 }
 
 IP_BODY(dsdn) {
@@ -98,11 +102,11 @@ IP_BODY(dsdn) {
     conv<MODE, RELU, G::S, EDGE, NBK>(tl, 1, id, a, true);                      // relu(bn1(conv1 x))
     conv<MODE, RELU | ADD_ID | SAVE_ID, G::S, EDGE, NBK>(tl, 1, id, a, b < 14); // relu(bn2(conv2 .) + x)
   }
-  double d[HEAD_ROWS];
+  double d[HeadOut<MODE, NBK>::ROWS];
   head<MODE, NBK>(tl, 1, d);
-  float o[HEAD_ROWS];
+  float o[HeadOut<MODE, NBK>::ROWS];
   round_rows(d, o);
-  store_out(tl, y, n, o, H, T);
+  store_out<MODE, NBK>(tl, y, n, o, H, T);
 }
 
 IP_BODY(pidn) {
@@ -120,13 +124,13 @@ IP_BODY(pidn) {
   }
   stem<MODE, true, NBK>(tl, 0);       // + identity (the stem output), recomputed from x
   __syncthreads();
-  double d[HEAD_ROWS];
+  double d[HeadOut<MODE, NBK>::ROWS];
   head<MODE, NBK>(tl, 1, d);
-  float o[HEAD_ROWS];
+  float o[HeadOut<MODE, NBK>::ROWS];
   round_rows(d, o);
 #pragma unroll
-  for (int k = 0; k < HEAD_ROWS; ++k) o[k] = 1.0f / (1.0f + expf(-o[k]));
-  store_out(tl, y, n, o, H, T);
+  for (int k = 0; k < HeadOut<MODE, NBK>::ROWS; ++k) o[k] = 1.0f / (1.0f + expf(-o[k]));
+  store_out<MODE, NBK>(tl, y, n, o, H, T);
 }
 
 // Short last tiles: the last tile of a spectrum holds only the positions left over by the full

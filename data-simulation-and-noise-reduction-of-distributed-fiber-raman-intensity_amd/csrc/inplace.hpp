@@ -427,38 +427,110 @@ __device__ __forceinline__ void stem(const Tile& tl, int slot) {
   }
 }
 
-// Conv1d(64, 1, 3, padding=1), one row per thread (row j = __builtin_amdgcn_workitem_id_x() + THREADS * k in out[k]),
-// fp32 weights and activations, fp64 accumulate: the 192-term sum is exact to ~1e-16 and rounded
-// once by the caller, after the network's own combine (RRCDNet x - (r + l)/2, RRCDNet/train.py:98,
-// a cancellation; PIDN/APIDN sigmoid).  ~400 fp64 FMAs per thread per network: negligible.
-constexpr int HEAD_ROWS = 2;      // rows per thread: ceil(640 / 512)
+// Conv1d(64, 1, 3, padding=1): the head, fp32 weights, fp64 or exact-ish accumulation, rounded once
+// by the caller after the network's own combine (RRCDNet x - (r + l)/2, RRCDNet/train.py:98, a
+// cancellation; PIDN/APIDN sigmoid).
+//
+// Row mapping of the results (HeadOut): fp32 / split-bf16 tiles, one row per thread (row tid + 512k
+// in out[k]); the 16-bit tiles (f16 + e4m3, single-plane f16/bf16), the B-fragment arrangement of the
+// convs -- lane (q, c16) of wave w reads the 16-B f16 slots 4u + q of rows 128k + 16w + c16 + t - 1
+// (conflict-free ds_read_b128, like the conv B reads, instead of per-row 8-B reads that hit the same
+// banks 4-way: the row-per-thread head cost 10 % of the f16 RRCDNet kernel), accumulates its 16
+// channels x 3 taps, and the 4 quarters are summed across lanes (v_permlane16/32_swap): out[k] is
+// row 128k + 16w + c16, on every quarter's lanes.
+constexpr int HEAD_ROWS = 2;      // rows per thread of the row-per-thread head: ceil(640 / 512)
+template <int MODE, int NBK = 4> struct HeadOut {
+  static constexpr bool VEC = MODE == MODE_H8 || single16(MODE);
+  static constexpr int ROWS = VEC ? NBK : HEAD_ROWS;
+  __device__ static int row(int k) {
+    const int t = __builtin_amdgcn_workitem_id_x();
+    return VEC ? 128 * k + 16 * (t >> 6) + (t & 15) : t + THREADS * k;
+  }
+  __device__ static bool writer() { return !VEC || (__builtin_amdgcn_workitem_id_x() & 48) == 0; }
+};
+
+__device__ __forceinline__ float quarter_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float h = __uint_as_float(a[0]) + __uint_as_float(a[1]);          // lanes l, l ^ 32
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(h), __float_as_uint(h), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);                   // and the other 16-lane row
+}
+
 template <int MODE, int NBK = 4>
-__device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[HEAD_ROWS]) {
+__device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[HeadOut<MODE, NBK>::ROWS]) {
   using TG = TileGeo<NBK>;
-  static_assert(TG::WB <= HEAD_ROWS * THREADS, "head rows per thread");
   const cfloat* hw = small_slot(tl, slot);
+  if constexpr (HeadOut<MODE, NBK>::VEC) {
+    const int tid = opaque_tid(), lane = tid & 63, w = tid >> 6, q = lane >> 4, c16 = lane & 15;
+    // channel of element jj of 16-B f16 slot s: h16_channel order (f16 + e4m3 tile), natural otherwise
+    auto chan = [&](int s, int jj) { return MODE == MODE_H8 ? h16_channel(s, jj) : 8 * s + jj; };
+    float wv[3][16];
+    const float* hwv = (const float*)hw;
 #pragma unroll
-  for (int k = 0; k < HEAD_ROWS; ++k) {
-  const int j = opaque_tid() + THREADS * k;
-  out[k] = 0.0;
-  if (j >= TG::WB) continue;
-  double a = (double)hw[192];
+    for (int t = 0; t < 3; ++t)
 #pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int prow = TG::row(j + t - 1);
+      for (int i = 0; i < 16; ++i) wv[t][i] = hwv[3 * chan(4 * (i >> 3) + q, i & 7) + t];
+    const float bias = hw[192];
+#pragma unroll
+    for (int k = 0; k < NBK; ++k) {
+      float acc = 0.f;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int pr = TG::row(128 * k + 16 * w + c16 + t - 1);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int sl = 4 * u + q;
+          f32x4 v0, v1;
+          if constexpr (MODE == MODE_H8) {
+            const f16x8 h = *(const f16x8*)(tl.lds + off_f32(pr, 16 * sl));
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 lo = *(const u32x2*)(tl.lds + off_f32(pr, 192 + 8 * sl));
+            v0 = __builtin_convertvector(__builtin_shufflevector(h, h, 0, 1, 2, 3), f32x4) + unpk_e4m3(lo.x) * H8_LO_DIV;
+            v1 = __builtin_convertvector(__builtin_shufflevector(h, h, 4, 5, 6, 7), f32x4) + unpk_e4m3(lo.y) * H8_LO_DIV;
+          } else {
+            typedef typename Op<MODE>::V8 V8;
+            const V8 h = *(const V8*)(tl.lds + off_f32(pr, 16 * sl));
+            v0 = __builtin_convertvector(__builtin_shufflevector(h, h, 0, 1, 2, 3), f32x4);
+            v1 = __builtin_convertvector(__builtin_shufflevector(h, h, 4, 5, 6, 7), f32x4);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            acc = fmaf(wv[t][8 * u + e], v0[e], acc);
+            acc = fmaf(wv[t][8 * u + 4 + e], v1[e], acc);
+          }
+        }
+      }
+      out[k] = (double)quarter_sum(acc) + (double)bias;
+    }
+  } else {
+    static_assert(TG::WB <= HEAD_ROWS * THREADS, "head rows per thread");
+#pragma unroll
+    for (int k = 0; k < HEAD_ROWS; ++k) {
+      const int j = opaque_tid() + THREADS * k;
+      out[k] = 0.0;
+#if defined(RDN_ABLATE_NOHEAD)        // diagnostic (tools/ablate.py): no head LDS traffic, wrong output
+      continue;
+#endif
+      if (j >= TG::WB) continue;
+      double a = (double)hw[192];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int prow = TG::row(j + t - 1);
 #pragma unroll 4
-    for (int cb = 0; cb < 16; ++cb) {
-      const f32x4 v = Op<MODE>::load4(tl.lds, prow, 4 * cb);
+        for (int cb = 0; cb < 16; ++cb) {
+          const f32x4 v = Op<MODE>::load4(tl.lds, prow, 4 * cb);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a = fma((double)hw[3 * (cb * 4 + i) + t], (double)v[i], a);
+          for (int i = 0; i < 4; ++i) a = fma((double)hw[3 * (cb * 4 + i) + t], (double)v[i], a);
+        }
+      }
+      out[k] = a;
     }
   }
-  out[k] = a;
-  }
 }
-__device__ __forceinline__ void round_rows(const double (&d)[HEAD_ROWS], float (&f)[HEAD_ROWS]) {
+template <int N>
+__device__ __forceinline__ void round_rows(const double (&d)[N], float (&f)[N]) {
 #pragma unroll
-  for (int k = 0; k < HEAD_ROWS; ++k) f[k] = (float)d[k];
+  for (int k = 0; k < N; ++k) f[k] = (float)d[k];
 }
 
 // LDS-only workgroup barrier: waits for this wave's LDS traffic, NOT for its outstanding global
@@ -915,10 +987,14 @@ __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const 
   return tl;
 }
 
-__device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, const float (&v)[HEAD_ROWS], int halo, int T) {
+template <int MODE, int NBK = 4>
+__device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, const float (&v)[HeadOut<MODE, NBK>::ROWS],
+                                          int halo, int T) {
+  using HO = HeadOut<MODE, NBK>;
+  if (!HO::writer()) return;
 #pragma unroll
-  for (int k = 0; k < HEAD_ROWS; ++k) {
-    const int j = opaque_tid() + THREADS * k;
+  for (int k = 0; k < HO::ROWS; ++k) {
+    const int j = HO::row(k);
     const int p = tl.base + j;
     if (j >= halo && j < halo + T && p < tl.L) y[(size_t)n * tl.L + p] = v[k];
   }

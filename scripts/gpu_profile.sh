@@ -1,7 +1,7 @@
 # Profiling pass for the round's evidence (profiles/): parity table, the headline bench under
 # rocprofv3 --kernel-trace --stats (the same default command the driver runs), and separate PMC
 # passes (FETCH_SIZE, WRITE_SIZE, SQ counters) per MI355X_MICROARCH.md §HBM / §PMC slots.
-# Afterwards, on the build host: python tools/summarize_profiles.py gpurun_out/prof profiles/r01
+# Afterwards, on the build host: python tools/summarize_profiles.py gpurun_out/prof profiles/rNN
 set +e
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -12,8 +12,8 @@ rc=$?; echo "parity rc=$rc"; if [ $rc -ne 0 ]; then tail -5 $OUT/parity.log; exi
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py > $OUT/kt_bench.log 2>&1
 rc=$?; echo "kt rc=$rc"; tail -1 $OUT/kt_bench.log | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi
 SHORT="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-variants --no-pipeline"
-for dt in f16f8 bf16x3 bf16; do
-  for ctr in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
+for dt in ${PROFILE_DTYPES:-f16 f16-plain f16f8}; do
+  for ctr in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM"; do
     tag=$(echo $ctr | cut -d' ' -f1)
     timeout -s KILL 150 rocprofv3 --pmc $ctr --output-format csv -d $OUT/pmc_${dt}_$tag -o p -- python3 $SHORT --dtype $dt > $OUT/pmc_${dt}_$tag.log 2>&1
     rc=$?; echo "pmc $dt $tag rc=$rc"; if [ $rc -ne 0 ]; then tail -3 $OUT/pmc_${dt}_$tag.log; exit $rc; fi
@@ -21,12 +21,3 @@ for dt in f16f8 bf16x3 bf16; do
 done
 timeout -k 10 400 python -u tools/throughput_table.py --out $OUT/throughput.md > $OUT/throughput.log 2>&1
 rc=$?; echo "throughput rc=$rc"; if [ $rc -ne 0 ]; then tail -3 $OUT/throughput.log; exit $rc; fi
-mkdir -p gpurun_out/unf
-for dt in fp32 bf16; do
-  timeout -k 10 240 python -u tools/unfused_baseline.py --dtype $dt --out gpurun_out/unf/unfused_$dt.json > gpurun_out/unf/unfused_$dt.log 2>&1
-  rc=$?; echo "unfused $dt rc=$rc"; if [ $rc -ne 0 ]; then tail -3 gpurun_out/unf/unfused_$dt.log; exit $rc; fi
-  for ctr in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 150 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/unf/pmc_${dt}_$ctr -o p -- python3 tools/unfused_baseline.py --dtype $dt --steps 2 --warmup 2 --batch 64 > gpurun_out/unf/pmc_${dt}_$ctr.log 2>&1
-    rc=$?; echo "pmc unfused $dt $ctr rc=$rc"; if [ $rc -ne 0 ]; then tail -3 gpurun_out/unf/pmc_${dt}_$ctr.log; exit $rc; fi
-  done
-done

@@ -24,7 +24,7 @@ VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "ntpipe": "-DRDN_IP_NTPIPE=1", "ntpipe0": "-DRDN_IP_NTPIPE=0", "fastsplit": "-DRDN_H8_FASTSPLIT=1",
             "hibase0": "-DRDN_IP_HIBASE=0", "dsdn3": "-DRDN_DSDN_NBK=3", "comp0": "-DRDN_F32_COMP=0",
             "chunk1": "-DRDN_F32_CHUNK=1", "chunk3": "-DRDN_F32_CHUNK=3", "chunk4": "-DRDN_F32_CHUNK=4",
-            "h16f16": "-DRDN_H16_F16=1", "h8plain": "-DRDN_ABLATE_H8_PLAIN"}
+            "h16f16": "-DRDN_H16_F16=1", "h8plain": "-DRDN_ABLATE_H8_PLAIN", "nohead": "-DRDN_ABLATE_NOHEAD"}
 
 
 def build():
@@ -33,7 +33,7 @@ def build():
     from concurrent.futures import ThreadPoolExecutor
     tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
     os.makedirs(OUT, exist_ok=True)
-    srcs = ["fused16.hip", "fused_inplace.hip", "cbam.hip", "generator.hip", "metrics.hip", "abi.cpp",
+    srcs = ["fused16.hip", "fused16_f16.hip", "fused_inplace.hip", "cbam.hip", "generator.hip", "metrics.hip", "abi.cpp",
             "pack.cpp"]
     only = sys.argv[2:]
     names = [n for n in VARIANTS if not only or n in only]
@@ -44,7 +44,7 @@ def build():
             o = os.path.join(OUT, f"{name}_{s}.o")
             cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mcode-object-version=5",
                    "-fno-gpu-rdc", "-c", os.path.join(CSRC, s), "-o", o] + flag.split()
-            if s in ("fused16.hip", "fused_inplace.hip", "cbam.hip") and name != "ieee":
+            if s in ("fused16.hip", "fused16_f16.hip", "fused_inplace.hip", "cbam.hip") and name != "ieee":
                 cmd += ["-fno-honor-nans", "-mno-amdgpu-ieee"]
             if s == "generator.hip":
                 cmd += ["-ffp-contract=off"]

@@ -34,7 +34,7 @@ def main():
         whichs = ["synth"] + (["trained"] if any(k.startswith("w::") for k in g.files) else [])
         for which in whichs:
             sd = golden_state_dict(arch, which)
-            for dtype in ("fp32", "f16f8", "bf16x3", "bf16-unsafe"):
+            for dtype in ("fp32", "f16", "f16-plain", "f16f8", "bf16x3", "bf16-unsafe"):
                 m = R.MODELS[arch]()
                 m.load_state_dict(sd)
                 m = m.cuda().eval().set_engine_dtype(dtype)

@@ -23,7 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--archs", nargs="*", default=["DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN"])
-    ap.add_argument("--dtypes", nargs="*", default=["f16f8", "bf16x3", "bf16-unsafe", "fp32"])
+    ap.add_argument("--dtypes", nargs="*", default=["f16", "f16-plain", "f16f8", "bf16x3", "bf16-unsafe", "fp32"])
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     import raman_mi355x as R
@@ -34,7 +34,7 @@ def main():
     for arch in args.archs:
         for L in ([10000, 16384] if arch in ("PIDN", "APIDN") else [10000]):
             for dt in args.dtypes:
-                B = {"bf16-unsafe": 4096, "bf16x3": 2048, "f16f8": 2048, "fp32": 1024}[dt]
+                B = {"f16": 4096, "f16-plain": 4096, "bf16-unsafe": 4096, "bf16x3": 2048, "f16f8": 2048, "fp32": 1024}[dt]
                 if arch in ("ADSDN", "APIDN"):
                     B //= 2
                 B = max(64, B * 10000 // L)
@@ -44,12 +44,12 @@ def main():
                 x = noisy.view(B, 1, L)
                 packed = m.packed_weights(dev)
                 y = torch.empty_like(x)
-                engine.forward(arch, dt, packed, x, out=y)
+                engine.forward(arch, m.engine_code, packed, x, out=y, check=False)
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(args.reps):
-                    engine.forward(arch, dt, packed, x, out=y)
+                    engine.forward(arch, m.engine_code, packed, x, out=y, check=False)
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / args.reps
