@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fiber-raman-intensity_amd"))
 sys.path.insert(0, ROOT)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -56,25 +57,102 @@ def flops_per_spectrum(arch, L):
     return per_pos * L
 
 
-def cpu_baseline(arch, L, seconds):
-    """The CPU oracle (fp32 PyTorch-CPU restatement, pinned to the reference by the golden
-    fixtures) in the reference evaluate loop shape: batch-1 forwards (evaulate.py:29-32)."""
-    from oracle.models import forward as oracle_forward
+def _cpu_model_name():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _reference_inputs(n, L):
+    """Spectra of the reference's own generator (oracle.refgen, bit-exact with 数据集产生.py:5-64),
+    seeded like config 1's data/test.npz."""
+    from oracle.refgen import generate_signals
+    state = np.random.get_state()
+    np.random.seed(20250410)
+    clean, noisy, _, _ = generate_signals(n, signal_length=L)
+    np.random.set_state(state)
+    return clean, noisy
+
+
+def _weights(arch):
+    """The trained golden state_dict (tests/golden; the reference ships no checkpoint), else random init."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    try:
+        from conftest import golden_state_dict, load_golden
+        if any(k.startswith("w::") for k in load_golden(arch).files):
+            return golden_state_dict(arch, "trained"), "trained golden fixture (tests/golden)"
+    except (ImportError, OSError):
+        pass
     import raman_mi355x as R
     torch.manual_seed(0)
-    sd = R.MODELS[arch]().state_dict()
-    x = torch.rand(1, 1, L)
-    oracle_forward(arch, sd, x)                  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        oracle_forward(arch, sd, torch.rand(1, 1, L))
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds and n >= 3:
-            break
-    return {"value": n / el, "unit": "spectra/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{n} batch-1 fp32 {arch} forwards at L={L} ({el:.1f} s, oracle.models on "
-                      f"{torch.get_num_threads()} threads, loop shape of evaulate.py:29-32)"}
+    return R.MODELS[arch]().state_dict(), "random init"
+
+
+def cpu_baseline(arch, L, seconds):
+    """The reference CPU path, restated (oracle.models: the reference's fp32 PyTorch-CPU ops, pinned to
+    the reference by the golden fixtures), in the evaulate.py:29-37 loop shape on the box's host cores:
+    batch-1 forwards without metrics (`value`), batch-1 with the per-spectrum metrics of
+    evaulate.py:34-37 (oracle.metrics: MSE, skimage-0.18.3 SSIM, Smoothness, Peak2Peak), and a
+    batched-16 forward loop (BASELINE.md CPU-baseline plan).  Bounded: ~`seconds` per variant."""
+    from oracle.metrics import per_spectrum
+    from oracle.models import forward as oracle_forward
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd, wsrc = _weights(arch)
+    clean, noisy = _reference_inputs(64, L)
+    xs = [torch.tensor(v, dtype=torch.float32).view(1, 1, -1) for v in noisy]
+    oracle_forward(arch, sd, xs[0])                  # warm-up
+
+    def loop(body):
+        n, t0 = 0, time.perf_counter()
+        while True:
+            body(n)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds and n >= 3:
+                return n, el
+
+    n1, e1 = loop(lambda i: oracle_forward(arch, sd, xs[i % len(xs)]))
+    n2, e2 = loop(lambda i: per_spectrum(oracle_forward(arch, sd, xs[i % len(xs)]).view(1, -1).numpy(),
+                                         clean[i % len(xs)][None]))
+    xb = torch.tensor(noisy[:16], dtype=torch.float32).unsqueeze(1)
+    n3, e3 = loop(lambda i: oracle_forward(arch, sd, xb))
+    return {"value": n1 / e1, "unit": "spectra/s", "cores": threads, "kind": "port",
+            "sample": f"{n1} batch-1 fp32 {arch} forwards at L={L} ({e1:.1f} s), evaulate.py:29-32 loop shape, "
+                      f"oracle.models (the reference's ops) on {threads} threads; weights: {wsrc}; inputs: the "
+                      "reference generator (oracle.refgen, seed 20250410)",
+            "with_metrics_spectra_per_s": n2 / e2,
+            "batched16_spectra_per_s": 16 * n3 / e3,
+            "host": {"cpu_model": _cpu_model_name(), "os_cpu_count": os.cpu_count(), "torch": torch.__version__}}
+
+
+def batch1_latency(model, code, arch, L, dev, n=200):
+    """The reference's evaluate loop shape through the drop-in module (evaulate.py:29-32): one spectrum
+    per forward.  `host_loop`: host array -> tensor -> device -> forward -> .cpu() per spectrum;
+    `device_resident`: input already on the GPU, forward + sync per spectrum."""
+    _, noisy = _reference_inputs(8, L)
+    with torch.no_grad():
+        for _ in range(3):
+            model(torch.tensor(noisy[0], dtype=torch.float32).view(1, 1, -1).to(dev)).cpu()
+        t0 = time.perf_counter()
+        for i in range(n):
+            model(torch.tensor(noisy[i % 8], dtype=torch.float32).unsqueeze(0).unsqueeze(0).to(dev)).cpu().squeeze().numpy()
+        host = (time.perf_counter() - t0) / n
+        xd = torch.tensor(noisy[0], dtype=torch.float32).view(1, 1, -1).to(dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(n):
+            model(xd)
+            torch.cuda.synchronize()
+        dres = (time.perf_counter() - t0) / n
+    return {"host_loop_ms_per_spectrum": host * 1e3, "host_loop_spectra_per_s": 1.0 / host,
+            "device_resident_ms_per_spectrum": dres * 1e3, "spectra": n, "L": L, "engine_dtype_code": code,
+            "note": "module forward at batch 1 (evaulate.py:29-32); per call: pack-cache key check, one fused launch"}
 
 
 def traffic_per_spectrum(arch, dtype):
@@ -153,9 +231,10 @@ def main():
     ap.add_argument("--batch", type=int, default=8192, help="spectra per GPU per step")
     ap.add_argument("--L", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=20250410)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline variant (3 variants)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true", help="skip timing the other engine dtypes")
+    ap.add_argument("--no-batch1", action="store_true", help="skip the batch-1 evaluate-loop latency")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip timing the simulate -> forward -> metrics pipeline (SURVEY.md §8d configs 3-4)")
     args = ap.parse_args()
@@ -229,6 +308,10 @@ def main():
                             "roofline_frac": flops_per_spectrum(args.arch, L) * nb / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[dt]}
         model.set_engine_dtype(args.dtype)
 
+    batch1 = None
+    if not args.no_batch1 and rank == 0:
+        batch1 = batch1_latency(model, code, args.arch, L, dev)
+
     pipeline = None
     if not args.no_pipeline:
         pipeline = time_pipeline(engine, args.arch, code, packed, args.seed, (world + rank) * B, B, L,
@@ -258,6 +341,7 @@ def main():
                                                         if mfma_cost(args.arch, args.dtype) else None)},
             "variants": variants,
             "pipeline": pipeline,
+            "batch1": batch1,
             "metrics_mean": {k: sums[i] / sums[4] for i, k in enumerate(["MSE", "SSIM", "Smoothness", "Peak2Peak"])},
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -14,7 +14,7 @@ noise, ...), so its streams cannot be reproduced per spectrum.  The engine inste
 Philox4x32-10 stream on (seed, spectrum index, draw tag, draw index) so that any index range can be
 generated independently on any GPU; this module reproduces those draws exactly (integer draws
 bit-exact, float transforms in the same float32 op order).  Parity with the reference itself is
-statistical (tests/test_generator_stats.py).
+statistical (tests/test_generator_gpu.py, against tests/golden/generator_stats.json).
 """
 import numpy as np
 

@@ -167,3 +167,20 @@ def test_bench_algorithmic_flops_match_survey():
         assert abs(bench.flops_per_spectrum(arch, 10000) - g) / g < 5e-5, arch
     assert abs(bench.flops_per_spectrum("PIDN", 16384) - 12.092e9) / 12.092e9 < 5e-4
     assert abs(bench.flops_per_spectrum("APIDN", 16384) - 12.099e9) / 12.099e9 < 5e-4
+
+
+def test_refgen_reproduces_reference_generator_bit_exact(inputs):
+    """oracle.refgen against the spectra the reference's own generate_signals produced for the fixtures
+    (tests/golden/make_golden.py: np.random.seed(20250410); gen(3); gen(2, L) for L in 7, 8, 33, 1000;
+    gen(1, 16384), in that order on one global stream)."""
+    from oracle.refgen import generate_signals
+    np.random.seed(20250410)
+    c, n, _, _ = generate_signals(3, signal_length=10000)
+    np.testing.assert_array_equal(c, inputs["main_clean64"])
+    np.testing.assert_array_equal(n, inputs["main_noisy64"])
+    for L in (7, 8, 33, 1000):
+        c, n, _, _ = generate_signals(2, signal_length=L, extreme_noise_prob=0.0 if L <= 100 else 0.05)
+        np.testing.assert_array_equal(n.astype(np.float32), inputs[f"edge{L}_noisy"])
+        np.testing.assert_array_equal(c.astype(np.float32), inputs[f"edge{L}_clean"])
+    c, n, _, _ = generate_signals(1, signal_length=16384)
+    np.testing.assert_array_equal(n.astype(np.float32), inputs["long_noisy"])
