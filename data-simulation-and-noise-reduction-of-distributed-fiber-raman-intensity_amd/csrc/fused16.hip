@@ -1,348 +1,11 @@
-// Whole-network fused tile kernels for the single-rounding 16-bit modes: RDN_F16 (this file compiled
-// with RDN_H16_F16=1, fused16_f16.hip: v_mfma_f32_16x16x32_f16, f16 weights and activations -- the
-// headline mode, within the 2e-2 bar on every golden fixture) and RDN_BF16 ('bf16-unsafe':
-// v_mfma_f32_16x16x32_bf16, bf16 -- NOT within 2e-2 on trained weights).  fp32 accumulation in both.
-// The two instantiations share every line below; only the element type, the MFMA and the namespace
-// (h16 / h16f, so rocprof tells them apart) differ.
-//
-// Geometry.  One workgroup = one tile of WB = 640 consecutive positions of one spectrum (its T
-// output positions plus a halo on each side).  LDS holds two ping-pong activation buffers of
-// 640 rows x 128 B (64 channels x bf16) = the CU's whole 160 KiB.  There are no guard rows: a tap
-// that falls off one end of the tile wraps to the other end.  Those rows lie outside every
-// output's receptive field (the halo covers the full depth of the stack), so any finite value
-// serves; positions outside [0, L) of the spectrum itself are re-zeroed by every epilogue — the
-// zero padding each reference Conv1d applies.
-//
-// Each Conv1d(64,64,3,d) is an implicit GEMM  Y[64 cout][640 pos] = W[64][192] . X~[192][640]
-// whose B operand is read straight from the activation buffer at row offsets (t-1)*d (no
-// im2col).  Wave w owns rows [RW*w, RW*w + RW) and ALL 64 output channels (4 M-tiles), so every
-// activation row is read from LDS once per tap; the layer's 24 A-fragments (24 KB of weights)
-// sit in VGPRs, loaded from L2, and the next layer's fragment (m, s) is fetched right after its
-// last use.  Accumulators start at the folded bias; ReLU (+ residual) and the bf16 rounding run in
-// an epilogue that trails the MFMA stream by one N-tile, and each N-tile is written back with two
-// ds_write_b128.  One LDS barrier per layer.
-//
-// Channel order inside an LDS row (= K order of the packed A-fragments, csrc/pack.cpp): 16-B slot
-// g = 4u + q holds channels h16_channel(g, j) = 32u + 4q + (j & 3) + 16 (j >> 2), j = 0..7 — the
-// 8 output channels lane quarter q of M-tiles 2u and 2u+1 holds after an MFMA (C/D map) AND the 8
-// K-elements lane quarter q of k-step (t, u) feeds in (B map).  Slots are XOR-swizzled by
-// (row & 7): B reads (ds_read_b128) and epilogue writes (ds_write_b128) are bank-conflict-free.
-//
-// Reference forwards: 1DCNN/train.py:71-82, RRCDNet/train.py:72-98, DSDN/train.py:72-126,
-// PIDN/train.py:72-106.
-#include "common.hpp"
+// Whole-network fused kernels and host launcher of the single-rounding 16-bit modes (device
+// building blocks: fused16.hpp).  Reference forwards: 1DCNN/train.py:71-82, RRCDNet/train.py:72-98,
+// DSDN/train.py:72-126, PIDN/train.py:72-106.
+#include "fused16.hpp"
 #include "host_util.hpp"
-
-#ifndef RDN_H16_F16
-#define RDN_H16_F16 0
-#endif
-#if RDN_H16_F16
-#define H16_NS h16f
-#define H16_LAUNCH launch_fused16_f16
-#define H16_ATTR_SLOT0 56
-#else
-#define H16_NS h16
-#define H16_LAUNCH launch_fused16
-#define H16_ATTR_SLOT0 0
-#endif
 
 namespace rdn {
 namespace H16_NS {
-
-constexpr int WB = H16_WB;                            // 640 rows per tile, halo included
-constexpr int ROWB = 128;                             // 64 channels x 16 bit
-constexpr uint32_t BUF_BYTES = WB * ROWB;             // 81920
-constexpr uint32_t LDS_BYTES = 2 * BUF_BYTES;         // 163840: the whole LDS of a CU
-constexpr uint32_t BUF0 = 0, BUF1 = BUF_BYTES;
-constexpr int LAYER_BYTES = BIG_BYTES_BF16;           // [m 4][k-step 6][lane 64][8 x 16 bit] + bias[64] f32
-constexpr int BIAS_OFF = BIG_FRAG_BYTES_BF16;
-#ifndef RDN_H16_WAVES
-#define RDN_H16_WAVES 8
-#endif
-#ifndef RDN_H16_PF
-#define RDN_H16_PF 2
-#endif
-constexpr int WAVES = RDN_H16_WAVES;
-constexpr int THREADS = 64 * WAVES;
-constexpr int RW = WB / WAVES;                        // rows per wave
-constexpr int NT = RW / 16;                           // 16-row N-tiles per wave
-static_assert(RW % 16 == 0, "rows per wave must be whole N-tiles");
-static_assert((WB % 64) == 0 && (THREADS % 64) == 0, "stem items must not straddle a slot within a wave");
-
-typedef float f32x8 __attribute__((ext_vector_type(8)));
-#if RDN_H16_F16
-typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
-typedef f16x8_t V;
-typedef _Float16 E;
-__device__ __forceinline__ f32x4 mma(V a, V b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
-#else
-typedef bf16x8 V;
-typedef __bf16 E;
-__device__ __forceinline__ f32x4 mma(V a, V b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
-#endif
-
-// Thread index the compiler cannot treat as loop-invariant (per-lane addresses are recomputed where
-// they are used instead of being hoisted across the network's layers and spilled)
-__device__ __forceinline__ int tid() {
-  int t = __builtin_amdgcn_workitem_id_x();
-  asm volatile("" : "+v"(t));
-  return t;
-}
-__device__ __forceinline__ int soff(int row, int slot) { return row * ROWB + ((slot ^ (row & 7)) << 4); }
-__device__ __forceinline__ int wrap(int row) { return row < 0 ? row + WB : (row >= WB ? row - WB : row); }
-__device__ __forceinline__ bool in_range(int p, int L) { return (unsigned)p < (unsigned)L; }
-// LDS-only workgroup barrier: this wave's LDS traffic drains, its global loads (next layer's
-// weights) stay in flight.  One asm statement, so no memory access moves across it.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-struct Tile {
-  char* lds;
-  const float* x;        // this spectrum
-  int L;
-  int base;              // spectrum position of tile row 0
-  const float* small;    // small section of the blob
-  const uint8_t* big;    // big-layer section
-  __amdgpu_buffer_rsrc_t wrsrc;   // buffer resource over the big-layer section (scalar-offset loads)
-  int layer;             // big layer whose fragments are in VGPRs
-};
-
-struct Frags {            // one layer's operands in VGPRs: A-fragments and folded bias
-  V a[4][6];
-  f32x4 bias[4];
-};
-
-// Operand loads as raw buffer loads: lane offset in a VGPR, layer/fragment offset in an SGPR, so
-// the 28 loads of a layer cost no address VALU.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ V load_frag(const Tile& tl, int layer, int m, int s) {
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, (tid() & 63) * 16,
-                                                        layer * LAYER_BYTES + (m * 6 + s) * 1024, 0);
-  return __builtin_bit_cast(V, v);
-}
-
-// lane quarter q's 4 output channels of M-tile m
-__device__ __forceinline__ f32x4 load_bias(const Tile& tl, int layer, int m) {
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, ((tid() & 63) >> 4) * 16,
-                                                        layer * LAYER_BYTES + BIAS_OFF + 64 * m, 0);
-  return __builtin_bit_cast(f32x4, v);
-}
-
-__device__ __forceinline__ void load_frags(const Tile& tl, int layer, Frags& F) {
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    F.bias[m] = load_bias(tl, layer, m);
-#pragma unroll
-    for (int s = 0; s < 6; ++s) F.a[m][s] = load_frag(tl, layer, m, s);
-  }
-}
-
-// Conv1d(1, 64, 3, padding=1) (+ folded BN) + ReLU in fp32: one (row, 16-B slot) item per lane,
-// 640 x 8 items over the workgroup (the slot is wave-uniform, so the weights are scalar loads).
-// ACCUM adds the result onto the resident row (PIDN/train.py:105, identity recomputed from x).
-template <bool ACCUM = false>
-__device__ __forceinline__ void stem(const Tile& tl, int sslot, uint32_t dst) {
-  const float* swp = tl.small + sslot * SMALL_SLOT_FLOATS;
-  asm volatile("" : "+s"(swp));      // no reuse of scalar-loaded weights across the layers in between
-  const cfloat* sw = (const cfloat*)swp;
-  for (int i = tid(); i < WB * 8; i += THREADS) {
-    const int g = __builtin_amdgcn_readfirstlane(i / WB);
-    const int row = i - g * WB;
-    const int p = tl.base + row;
-    const float xm = in_range(p - 1, tl.L) ? tl.x[p - 1] : 0.f;
-    const float x0 = in_range(p, tl.L) ? tl.x[p] : 0.f;
-    const float xp = in_range(p + 1, tl.L) ? tl.x[p + 1] : 0.f;
-    const bool valid = in_range(p, tl.L);
-    V* ptr = (V*)(tl.lds + dst + soff(row, g));
-    V v;
-    if (ACCUM) v = *ptr;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = h16_channel(g, j);
-      float a = sw[192 + c];
-      a = fmaf(sw[3 * c + 0], xm, a);
-      a = fmaf(sw[3 * c + 1], x0, a);
-      a = fmaf(sw[3 * c + 2], xp, a);
-      a = fmaxf(a, 0.f);
-      if (ACCUM) a += (float)v[j];
-      v[j] = (E)(valid ? a : 0.f);
-    }
-    *ptr = v;
-  }
-}
-
-enum Epi : int {
-  RELU = 0,       // relu(acc + b)
-  LINEAR = 1,     // acc + b                (PIDN block output: BN without ReLU)
-  RES_RELU = 2,   // relu(acc + b + dst)    (DSDN ResidualBlock: out += identity; relu)
-};
-
-// LDS byte addresses of this lane's B fragment for k-step s = (tap t, half u) of N-tile n.
-struct BAddr {
-  int m[6], first[2], last[2];
-  __device__ __forceinline__ BAddr(uint32_t src, int r0, int dil, int q) {
-#pragma unroll
-    for (int s = 0; s < 6; ++s) m[s] = (int)src + soff(r0 + ((s >> 1) - 1) * dil, 4 * (s & 1) + q);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      first[u] = (int)src + soff(wrap(r0 - dil), 4 * u + q);
-      last[u] = (int)src + soff(wrap(r0 + 16 * (NT - 1) + dil), 4 * u + q);
-    }
-  }
-  // N-tiles add 16 rows (2 KiB, swizzle unchanged); only (n = 0, t = 0) and (n = NT-1, t = 2)
-  // can leave the tile, and only in the first / last wave.
-  __device__ __forceinline__ int at(int n, int s) const {
-    const int t = s >> 1, u = s & 1;
-    if (n == 0 && t == 0) return first[u];
-    if (n == NT - 1 && t == 2) return last[u];
-    return m[s] + n * 16 * ROWB;
-  }
-};
-
-// One Conv1d(64, 64, 3, dilation=dil, padding=dil) over the tile, src -> dst.  NM = 4, or 1 for
-// the head (Conv1d(64, 1, 3) packed as a big layer whose output rows 1..63 are zero); the head
-// returns cout 0 of position w*RW + 16n + lane in out[n] of lanes 0..15.
-template <int EPI, int NM, bool EDGE>
-__device__ __forceinline__ void conv(Tile& tl, uint32_t src, uint32_t dst, int dil, Frags& F, bool has_next,
-                                     float (&out)[NT]) {
-  const int lane = tid() & 63, w = tid() >> 6, q = lane >> 4, c16 = lane & 15;
-  const int r0 = w * RW + c16;
-  const int next = tl.layer + 1;
-  const BAddr ba(src, r0, dil, q);
-  int sa[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) sa[u] = (int)dst + soff(r0, 4 * u + q);
-  const int pos0 = tl.base + w * RW;
-
-  // Idle waves of a short last tile: every row of this wave lies at position >= L + 2, beyond the
-  // reach (d <= 2) of any row that matters, so it skips the layer (its dst rows are never read by
-  // a stored output: positions L, L + 1 are re-zeroed by the wave that owns them, and the wrapped
-  // taps of rows 0, 1 erode into the halo like any other edge).  Its SIMD partner wave then has the
-  // MFMA pipe to itself.  It still fetches the next layer's operands and meets the barrier.
-  if (EDGE && __builtin_amdgcn_readfirstlane(pos0) >= tl.L + 2) {
-    if (has_next) load_frags(tl, next, F);
-#pragma unroll
-    for (int n = 0; n < NT; ++n) out[n] = 0.f;
-    tl.layer += 1;
-    if (NM == 4) lds_barrier();
-    return;
-  }
-
-  // bias (+ identity), ReLU, zero rows outside [0, L), round to bf16, store the 8 channels of
-  // M-tiles 2u, 2u+1 as one 16-B slot
-  auto epilogue = [&](int n, int u, const f32x4 (&acc)[NM]) {
-    const bool valid = !EDGE || in_range(pos0 + 16 * n + c16, tl.L);
-    f32x8 v = __builtin_shufflevector(acc[2 * u], acc[2 * u + 1], 0, 1, 2, 3, 4, 5, 6, 7);
-    V* p = (V*)(tl.lds + sa[u] + n * 16 * ROWB);
-    if (EPI == RES_RELU) v += __builtin_convertvector(*p, f32x8);
-    if (EPI != LINEAR) v = __builtin_elementwise_max(v, (f32x8)(0.f));
-    if (EDGE && !valid) v = (f32x8)(0.f);
-#if defined(RDN_ABLATE_NOSTORE)            // diagnostic builds only (tools/ablate.py)
-    if (v[0] == 123456.f)
-#endif
-    *p = __builtin_convertvector(v, V);
-  };
-
-  f32x4 prev[NM];
-  constexpr int PF = RDN_H16_PF;       // B fragments in flight ahead of the k-step that computes
-  V B[PF + 1];
-#pragma unroll
-  for (int k = 0; k < PF; ++k) B[k] = *(const V*)(tl.lds + ba.at(k / 6, k % 6));
-#pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    f32x4 acc[NM];
-#pragma unroll
-    for (int m = 0; m < NM; ++m) acc[m] = F.bias[m];
-    if (n == NT - 1 && has_next) {                            // last use of the bias in this layer
-#pragma unroll
-      for (int m = 0; m < 4; ++m) F.bias[m] = load_bias(tl, next, m);
-    }
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int k = 6 * n + s, kp = k + PF;
-#if defined(RDN_ABLATE_NOLDS)
-      if (kp < 6 * NT) { B[kp % (PF + 1)] = B[(k + 1) % (PF + 1)]; asm volatile("" : "+v"(B[kp % (PF + 1)])); }
-#else
-      if (kp < 6 * NT) B[kp % (PF + 1)] = *(const V*)(tl.lds + ba.at(kp / 6, kp % 6));
-#endif
-      const V b = B[k % (PF + 1)];
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-#if defined(RDN_ABLATE_NOMFMA)
-        asm volatile("" : "+v"(acc[m]) : "v"(F.a[m][s]), "v"(b));
-#else
-        acc[m] = mma(F.a[m][s], b, acc[m]);
-#endif
-      }
-#if defined(RDN_ABLATE_NOALOAD)
-      if (false) {
-#else
-      if (n == NT - 1 && has_next) {                          // last use of a[.][s] in this layer
-#endif
-#pragma unroll
-        for (int m = 0; m < 4; ++m) F.a[m][s] = load_frag(tl, next, m, s);
-      }
-      if (NM == 4 && n > 0 && (s == 1 || s == 3)) epilogue(n - 1, s >> 1, prev);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // head: M-row 0 holds f16/bf16(W), M-row 1 the rounding residue W - hi (pack.cpp
-    // pack_big_bf16): the two partial sums add in fp32, so the head's weights are exact to ~2^-22
-    // at no extra MFMA (the head's output feeds the RRCDNet cancellation x - (r + l)/2)
-    if (NM == 1) out[n] = acc[0][0] + acc[0][1];
-#pragma unroll
-    for (int m = 0; m < NM; ++m) prev[m] = acc[m];
-  }
-  if (NM == 4) {
-    epilogue(NT - 1, 0, prev);
-    epilogue(NT - 1, 1, prev);
-  }
-  tl.layer += 1;
-#if defined(RDN_ABLATE_NOBARRIER)
-  if (NM == 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
-  if (NM == 4) lds_barrier();
-#endif
-}
-
-template <int EPI, bool EDGE>
-__device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int dil, Frags& F, bool has_next = true) {
-  float unused[NT];
-  conv<EPI, 4, EDGE>(tl, src, dst, dil, F, has_next, unused);
-}
-
-template <bool EDGE>
-__device__ __forceinline__ void head(Tile& tl, uint32_t src, Frags& F, bool has_next, float (&out)[NT]) {
-  conv<LINEAR, 1, EDGE>(tl, src, src, 1, F, has_next, out);
-}
-
-__device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const float* x, int L, int T, int tiles,
-                                          int halo, int& n_out) {
-  const int n = __builtin_amdgcn_workgroup_id_x() / tiles, tile = __builtin_amdgcn_workgroup_id_x() - n * tiles;
-  n_out = n;
-  Tile tl;
-  tl.lds = lds;
-  tl.x = x + (size_t)n * L;
-  tl.L = L;
-  tl.base = tile * T - halo;
-  tl.small = (const float*)blob;
-  tl.big = blob + SMALL_BYTES;
-  // raw buffer over the big-layer section (stride 0, 2 GiB bound; dword 3 = 0x00020000, the raw
-  // 32-bit data format of the gfx9 buffer descriptor)
-  tl.wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)tl.big, 0, 0x7fffffff, 0x00020000);
-  tl.layer = 0;
-  return tl;
-}
-
-__device__ __forceinline__ int head_row(int k) { return (tid() >> 6) * RW + 16 * k + (tid() & 15); }
-
-__device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, const float (&v)[NT], int halo, int T) {
-  if ((tid() & 63) >= 16) return;
-#pragma unroll
-  for (int k = 0; k < NT; ++k) {
-    const int j = head_row(k);
-    const int p = tl.base + j;
-    if (j >= halo && j < halo + T && p < tl.L) y[(size_t)n * tl.L + p] = v[k];
-  }
-}
 
 // Network bodies; EDGE: the tile holds positions outside [0, L) (first/last tile of a spectrum),
 // whose rows every epilogue re-zeroes.  Interior tiles skip that per-row select.

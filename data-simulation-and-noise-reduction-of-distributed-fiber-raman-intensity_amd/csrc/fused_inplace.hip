@@ -5,6 +5,13 @@
 // PIDN/train.py:72-106.
 #include "inplace.hpp"
 #include "host_util.hpp"
+// the f16 ping-pong layers of fused16.hpp over the f16 + e4m3 blob (its leading f16 fragments):
+// the plain layers of RDN_F16MIX (rrcdnet_hybrid below)
+#define RDN_H16_F16 1
+#define H16_NS h16x
+#define H16_LAYER_BYTES BIG_BYTES_H8
+#define H16_BIAS_OFF H8_BIAS_OFF
+#include "fused16.hpp"
 
 namespace rdn {
 namespace ip {
@@ -149,6 +156,103 @@ IP_BODY(pidn) {
 // RDN_F16MIX: corrected layers at the end of RRCDNet's right branch (pack.cpp f16mix_default_mask)
 constexpr int RRCDNET_F16MIX_TAIL = 3;
 
+// RDN_F16MIX on full tiles: the plain f16 layers run on fused16's ping-pong tile (two 640 x 128-B
+// buffers, one barrier per layer, no write-back lag: 8 % fewer cycles per layer than the in-place
+// tile's f16 plane), then the activations move once into the in-place tile for the layers the
+// e4m3 planes serve (the producer of the corrected tail, the tail itself, the last left layer) and
+// the two heads, which read the f16 + e4m3-lo planes (HeadOut, vectorized).  The big-layer
+// fragments of the H8 blob start with fused16's [m][k-step][lane][8 x f16] map (pack.cpp
+// pack_big_h8 / pack_big_bf16, same h16_channel K order), so both halves read one blob.
+
+// ping-pong buffer `src` (640 rows x 128 B, fused16 slot swizzle) -> the f16 plane of the in-place
+// tile (640 rows x 256 B, off_f32 swizzle).  The two overlap: everything is read before anything
+// is written.
+__device__ __forceinline__ void pingpong_to_tile(char* lds, uint32_t src) {
+  constexpr int ITEMS = h16x::WB * 8 / THREADS;          // 10 (row, slot) items per thread
+  static_assert(h16x::WB * 8 % THREADS == 0 && h16x::WB == TileGeo<5>::WB, "one 640-row tile");
+  const int t = opaque_tid();
+  f16x8 v[ITEMS];
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const int item = t + THREADS * i, row = item >> 3, slot = item & 7;
+    v[i] = *(const f16x8*)(lds + src + h16x::soff(row, slot));
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const int item = t + THREADS * i, row = item >> 3, slot = item & 7;
+    *(f16x8*)(lds + off_f32(row, 16 * slot)) = v[i];
+  }
+  __syncthreads();
+}
+
+template <bool EDGE, int TAIL>
+__device__ __forceinline__ void rrcdnet_hybrid_body(Tile& tl, const uint8_t* blob, const float* x, float* y, int n,
+                                                    int L, int T, int tiles) {
+  constexpr int H = fused_halo(RRCDNET), NBK = 5, PP = 14 - TAIL;   // ping-pong layers of the right branch
+  using HO = HeadOut<MODE_H8, NBK>;
+  int n16;
+  h16x::Tile t16 = h16x::make_tile(tl.lds, blob, x, L, T, tiles, H, n16);
+  h16x::Frags F;
+  h16x::load_frags(t16, 0, F);
+  h16x::stem(t16, 0, h16x::BUF0);
+  h16x::lds_barrier();
+  uint32_t cur = h16x::BUF0, nxt = h16x::BUF1;
+  for (int i = 0; i < PP; ++i) {
+    h16x::layer<h16x::RELU, EDGE>(t16, cur, nxt, 1, F, i + 1 < PP);
+    const uint32_t s = cur; cur = nxt; nxt = s;
+  }
+  f32x4 id[16 * NBK / 4];
+  LayerA<MODE_H8> a;
+  tl.layer = PP;
+  load_layer_a<MODE_H8>(tl, PP, a);
+  pingpong_to_tile(tl.lds, cur);
+  conv<MODE_H8, RELU, 1, EDGE, NBK, false, true, true>(tl, 1, id, a, true);       // writes the e4m3 planes
+  for (int i = 0; i < TAIL; ++i) conv<MODE_H8, RELU, 1, EDGE, NBK, true, true, true>(tl, 1, id, a, i + 1 < TAIL);
+  double r[HO::ROWS];
+  head<MODE_H8, NBK>(tl, 2, r);
+  // left branch: layers 15-27 ping-pong, 28 in place (it writes the e4m3 lo plane the head reads)
+  t16.layer = 15;
+  h16x::load_frags(t16, 15, F);
+  __syncthreads();               // the left stem overwrites the rows the right head just read
+  h16x::stem(t16, 1, h16x::BUF0);
+  h16x::lds_barrier();
+  cur = h16x::BUF0; nxt = h16x::BUF1;
+  for (int i = 0; i < 13; ++i) {
+    h16x::layer<h16x::RELU, EDGE>(t16, cur, nxt, i == 7 ? 1 : 2, F, i + 1 < 13);
+    const uint32_t s = cur; cur = nxt; nxt = s;
+  }
+  tl.layer = 28;
+  load_layer_a<MODE_H8>(tl, 28, a);
+  pingpong_to_tile(tl.lds, cur);
+  conv<MODE_H8, RELU, 1, EDGE, NBK, false, true, false>(tl, 2, id, a, false);
+  double l[HO::ROWS];
+  head<MODE_H8, NBK>(tl, 3, l);
+  float o[HO::ROWS];
+#pragma unroll
+  for (int k = 0; k < HO::ROWS; ++k) {      // x - (r + l)/2 from the unrounded heads, one rounding
+    const int p = tl.base + HO::row(k);
+    const float xv = in_range(p, L) ? tl.x[p] : 0.f;
+    o[k] = (float)((double)xv - (r[k] + l[k]) * 0.5);
+  }
+  store_out<MODE_H8, NBK>(tl, y, n, o, H, T);
+}
+
+// RDN_F16MIX RRCDNet: hybrid bodies on 640-row tiles, the in-place body on short last tiles
+template <int TAIL>
+__global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restrict__ blob, const float* __restrict__ x,
+                                                          float* __restrict__ y, int L, int T, int tiles) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int n;
+  Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
+  const int need = L - tl.base + 2;
+  if (tl.base >= 0 && tl.base + TileGeo<5>::WB <= L) rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles);
+  else if (need <= 256) rrcdnet_body<MODE_H8, true, 2, TAIL>(tl, y, n, L, T);
+  else if (need <= 384) rrcdnet_body<MODE_H8, true, 3, TAIL>(tl, y, n, L, T);
+  else if (need <= 512) rrcdnet_body<MODE_H8, true, 4, TAIL>(tl, y, n, L, T);
+  else rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles);
+}
+
 #define IP_KERNEL(name, arch)                                                                              \
   template <int MODE, int TAIL = 0>                                                                         \
   __global__ __launch_bounds__(THREADS) void name(const uint8_t* __restrict__ blob, const float* __restrict__ x, \
@@ -173,6 +277,14 @@ IP_KERNEL(pidn, PIDN)
 
 }  // namespace ip
 
+#ifndef RDN_F16MIX_HYBRID
+#define RDN_F16MIX_HYBRID 1
+#endif
+#if RDN_F16MIX_HYBRID
+#define RDN_F16MIX_KERNEL ip::rrcdnet_hybrid<ip::RRCDNET_F16MIX_TAIL>
+#else
+#define RDN_F16MIX_KERNEL ip::rrcdnet<ip::MODE_H8, ip::RRCDNET_F16MIX_TAIL>
+#endif
 typedef void (*fused_kernel_t)(const uint8_t*, const float*, float*, int, int, int);
 
 template <int MODE>
@@ -192,7 +304,7 @@ hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const 
   if (arch < 0 || arch >= 8 || dtype < 0 || dtype > F16MIX) return hipErrorInvalidValue;
   const fused_kernel_t k = dtype == BF16X3 ? pick<ip::MODE_X3>(arch)
                            : dtype == F16F8 ? pick<ip::MODE_H8>(arch)
-                           : dtype == F16MIX ? (arch == RRCDNET ? ip::rrcdnet<ip::MODE_H8, ip::RRCDNET_F16MIX_TAIL> : nullptr)
+                           : dtype == F16MIX ? (arch == RRCDNET ? RDN_F16MIX_KERNEL : nullptr)
                            : dtype == F32   ? pick<ip::MODE_F32>(arch) : nullptr;
   if (!k) return hipErrorInvalidValue;
   const int nbk = arch == DSDN ? ip::NetGeo<DSDN>::NBK : ip::NetGeo<RRCDNET>::NBK;

@@ -24,7 +24,8 @@ VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "ntpipe": "-DRDN_IP_NTPIPE=1", "ntpipe0": "-DRDN_IP_NTPIPE=0", "fastsplit": "-DRDN_H8_FASTSPLIT=1",
             "hibase0": "-DRDN_IP_HIBASE=0", "dsdn3": "-DRDN_DSDN_NBK=3", "comp0": "-DRDN_F32_COMP=0",
             "chunk1": "-DRDN_F32_CHUNK=1", "chunk3": "-DRDN_F32_CHUNK=3", "chunk4": "-DRDN_F32_CHUNK=4",
-            "h16f16": "-DRDN_H16_F16=1", "h8plain": "-DRDN_ABLATE_H8_PLAIN", "nohead": "-DRDN_ABLATE_NOHEAD"}
+            "h16f16": "-DRDN_H16_F16=1", "h8plain": "-DRDN_ABLATE_H8_PLAIN", "nohead": "-DRDN_ABLATE_NOHEAD",
+            "mixold": "-DRDN_F16MIX_HYBRID=0", "pkrelu0": "-DRDN_H16_PKRELU=0"}
 
 
 def build():
@@ -40,22 +41,28 @@ def build():
     jobs = []
     for name in names:
         flag = VARIANTS[name]
+        # "prev": the sources of another tree (ABLATE_PREV_SRC = its csrc directory, e.g. a git archive of
+        # the last commit) for an A/B against the working tree in one process
+        src_dir = os.environ.get("ABLATE_PREV_SRC", CSRC) if name == "prev" else CSRC
         for s in srcs:
+            if not os.path.exists(os.path.join(src_dir, s)):
+                continue
             o = os.path.join(OUT, f"{name}_{s}.o")
             cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mcode-object-version=5",
-                   "-fno-gpu-rdc", "-c", os.path.join(CSRC, s), "-o", o] + flag.split()
+                   "-fno-gpu-rdc", "-c", os.path.join(src_dir, s), "-o", o] + flag.split()
             if s in ("fused16.hip", "fused16_f16.hip", "fused_inplace.hip", "cbam.hip") and name != "ieee":
                 cmd += ["-fno-honor-nans", "-mno-amdgpu-ieee"]
             if s == "generator.hip":
                 cmd += ["-ffp-contract=off"]
             jobs.append(cmd)
     with ThreadPoolExecutor(int(os.environ.get("ABLATE_JOBS", "8"))) as ex:
-        for r in ex.map(lambda c: subprocess.run(c, cwd=CSRC, capture_output=True, text=True), jobs):
+        for r in ex.map(lambda c: subprocess.run(c, cwd=os.path.dirname(c[c.index("-c") + 1]), capture_output=True,
+                                                 text=True), jobs):
             if r.returncode:
                 print(r.stderr[-3000:])
                 raise SystemExit("compile failed")
     for name in names:
-        objs = [os.path.join(OUT, f"{name}_{s}.o") for s in srcs]
+        objs = [os.path.join(OUT, f"{name}_{s}.o") for s in srcs if os.path.exists(os.path.join(OUT, f"{name}_{s}.o"))]
         subprocess.run(["g++", "-shared", "-o", os.path.join(OUT, f"lib_{name}.so")] + objs +
                        [f"-L{tlib}", "-l:libamdhip64.so", f"-Wl,-rpath,{tlib}"], check=True)
         print("built", name, flush=True)
