@@ -23,7 +23,7 @@ H16_BODY(denoisecnn) {
     layer<RELU, EDGE>(tl, cur, nxt, 1, F);
     const uint32_t t = cur; cur = nxt; nxt = t;
   }
-  float o[NT];
+  float o[HN];
   head<EDGE>(tl, cur, F, false, o);
   store_out(tl, y, n, o, H, T);
 }
@@ -42,7 +42,7 @@ H16_BODY(rrcdnet) {
     const uint32_t t = cur; cur = nxt; nxt = t;
   }
   {
-    float r[NT];
+    float r[HN];
     head<EDGE>(tl, cur, F, true, r);
     store_out(tl, y, n, r, H, T);   // parked in the output (re-read below): no VGPRs held across the left branch
   }
@@ -54,12 +54,12 @@ H16_BODY(rrcdnet) {
     layer<RELU, EDGE>(tl, cur, nxt, i == 7 ? 1 : 2, F);
     const uint32_t t = cur; cur = nxt; nxt = t;
   }
-  float l[NT];
+  float l[HN];
   head<EDGE>(tl, cur, F, false, l);
   // y = x - (right + left) / 2 on this tile's output rows (the lanes that stored r re-read it)
   if ((tid() & 63) < 16) {
 #pragma unroll
-    for (int k = 0; k < NT; ++k) {
+    for (int k = 0; k < HN; ++k) {
       const int j = head_row(k);
       const int p = tl.base + j;
       if (j >= H && j < H + T && p < L) {
@@ -83,7 +83,7 @@ H16_BODY(dsdn) {
     layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F);         // relu(bn1(conv1 x))
     layer<RES_RELU, EDGE>(tl, BUF1, BUF0, 1, F);     // relu(bn2(conv2 .) + x), written over x in place
   }
-  float o[NT];
+  float o[HN];
   head<EDGE>(tl, BUF0, F, false, o);
   store_out(tl, y, n, o, H, T);
 }
@@ -101,10 +101,10 @@ H16_BODY(pidn) {
   }
   stem<true>(tl, 0, BUF0);       // + identity (the stem output), recomputed in fp32 from x
   lds_barrier();
-  float o[NT];
+  float o[HN];
   head<EDGE>(tl, BUF0, F, false, o);
 #pragma unroll
-  for (int k = 0; k < NT; ++k) o[k] = 1.0f / (1.0f + expf(-o[k]));
+  for (int k = 0; k < HN; ++k) o[k] = 1.0f / (1.0f + expf(-o[k]));
   store_out(tl, y, n, o, H, T);
 }
 

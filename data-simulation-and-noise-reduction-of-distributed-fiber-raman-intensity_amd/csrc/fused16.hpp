@@ -15,12 +15,17 @@
 //
 // Each Conv1d(64,64,3,d) is an implicit GEMM  Y[64 cout][640 pos] = W[64][192] . X~[192][640]
 // whose B operand is read straight from the activation buffer at row offsets (t-1)*d (no
-// im2col).  Wave w owns rows [RW*w, RW*w + RW) and ALL 64 output channels (4 M-tiles), so every
-// activation row is read from LDS once per tap; the layer's 24 A-fragments (24 KB of weights)
-// sit in VGPRs, loaded from L2, and the next layer's fragment (m, s) is fetched right after its
-// last use.  Accumulators start at the folded bias; ReLU (+ residual) and the bf16 rounding run in
-// an epilogue that trails the MFMA stream by one N-tile, and each N-tile is written back with two
-// ds_write_b128.  One LDS barrier per layer.
+// im2col).  Wave w owns row block w % 4 (RW = 160 rows, NT = 10 N-tiles) and output channels
+// 32h .. 32h+31 (h = w / 4: two M-tiles), so the two waves of a SIMD (w, w + 4) split the output
+// channels of the same rows.  The split halves the weights a wave holds (12 A-fragments, 12 KB per
+// layer, loaded from L2/L1 by every wave: 96 KB per CU per layer instead of 192 KB -- the vector
+// memory path, not the MFMA, bounded the all-channels-per-wave layout) at the price of twice the
+// LDS B reads (480 KB per CU per layer at 256 B/clk: half the MFMA time).  The k-steps are the
+// OUTER loop: fragment (m, s) is dead after k-step s, so the next layer's copy is fetched right
+// there and the weight traffic spreads evenly over the layer (no burst at its end), while the
+// NT x 2 accumulators (80 VGPRs) stay live.  Accumulators start at the folded bias; ReLU
+// (+ residual) and the rounding run in an epilogue that trails the last k-step's MFMAs by one
+// N-tile, one ds_write_b128 per N-tile.  One LDS barrier per layer.
 //
 // Channel order inside an LDS row (= K order of the packed A-fragments, csrc/pack.cpp): 16-B slot
 // g = 4u + q holds channels h16_channel(g, j) = 32u + 4q + (j & 3) + 16 (j >> 2), j = 0..7 — the
@@ -65,20 +70,20 @@ constexpr uint32_t LDS_BYTES = 2 * BUF_BYTES;         // 163840: the whole LDS o
 constexpr uint32_t BUF0 = 0, BUF1 = BUF_BYTES;
 constexpr int LAYER_BYTES = H16_LAYER_BYTES;          // [m 4][k-step 6][lane 64][8 x 16 bit] ... bias[64] f32
 constexpr int BIAS_OFF = H16_BIAS_OFF;
-#ifndef RDN_H16_WAVES
-#define RDN_H16_WAVES 8
-#endif
 #ifndef RDN_H16_PF
-#define RDN_H16_PF 2
+#define RDN_H16_PF 5
 #endif
 #ifndef RDN_H16_PKRELU
 #define RDN_H16_PKRELU 1
 #endif
-constexpr int WAVES = RDN_H16_WAVES;
+constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
-constexpr int RW = WB / WAVES;                        // rows per wave
-constexpr int NT = RW / 16;                           // 16-row N-tiles per wave
-static_assert(RW % 16 == 0, "rows per wave must be whole N-tiles");
+constexpr int MH = 2;                                 // output-channel halves (2 M-tiles each)
+constexpr int RB = WAVES / MH;                        // row blocks
+constexpr int RW = WB / RB;                           // 160 rows per wave
+constexpr int NT = RW / 16;                           // 10 N-tiles per wave
+constexpr int HN = NT / MH;                           // head N-tiles per wave (the two halves split the rows)
+static_assert(RW % 16 == 0 && NT % MH == 0, "rows per wave must be whole N-tiles");
 static_assert((WB % 64) == 0 && (THREADS % 64) == 0, "stem items must not straddle a slot within a wave");
 
 typedef float f32x8 __attribute__((ext_vector_type(8)));
@@ -118,15 +123,17 @@ struct Tile {
   int layer;             // big layer whose fragments are in VGPRs
   // per-lane LDS offsets, computed once per tile (no address arithmetic at each layer's start):
   // koff[d + 2][u] = soff(r0 + d, 4u + q) for tap shift d in -2..2 (no wrap), r0 = this lane's
-  // first row (w * RW + lane % 16)
+  // first row ((w % RB) * RW + lane % 16)
   int koff[5][2];
   int r0;
 };
 
-struct Frags {            // one layer's operands in VGPRs: A-fragments and folded bias
-  V a[4][6];
-  f32x4 bias[4];
+struct Frags {            // one layer's operands in VGPRs: this wave's 2 M-tiles of A-fragments and folded bias
+  V a[2][6];
+  f32x4 bias[2];
 };
+// this wave's output-channel half (M-tiles 2h, 2h + 1), wave-uniform
+__device__ __forceinline__ int mhalf() { return __builtin_amdgcn_readfirstlane(tid() >> 6) / RB; }
 
 // Operand loads as raw buffer loads: lane offset in a VGPR, layer/fragment offset in an SGPR, so
 // the 28 loads of a layer cost no address VALU.
@@ -145,12 +152,12 @@ __device__ __forceinline__ f32x4 load_bias(const Tile& tl, int layer, int m, int
 }
 
 __device__ __forceinline__ void load_frags(const Tile& tl, int layer, Frags& F) {
-  const int lane = tid() & 63, fv = lane * 16, bv = (lane >> 4) * 16;
+  const int lane = tid() & 63, fv = lane * 16, bv = (lane >> 4) * 16, mt = 2 * mhalf();
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    F.bias[m] = load_bias(tl, layer, m, bv);
+  for (int m = 0; m < 2; ++m) {
+    F.bias[m] = load_bias(tl, layer, mt + m, bv);
 #pragma unroll
-    for (int s = 0; s < 6; ++s) F.a[m][s] = load_frag(tl, layer, m, s, fv);
+    for (int s = 0; s < 6; ++s) F.a[m][s] = load_frag(tl, layer, mt + m, s, fv);
   }
 }
 
@@ -223,131 +230,158 @@ struct BAddr {
   }
 };
 
-// One Conv1d(64, 64, 3, dilation=dil, padding=dil) over the tile, src -> dst.  NM = 4, or 1 for
-// the head (Conv1d(64, 1, 3) packed as a big layer whose output rows 1..63 are zero); the head
-// returns cout 0 of position w*RW + 16n + lane in out[n] of lanes 0..15.
-template <int EPI, int NM, bool EDGE>
-__device__ __forceinline__ void conv(Tile& tl, uint32_t src, uint32_t dst, int dil, Frags& F, bool has_next,
-                                     float (&out)[NT]) {
-  const int lane = tid() & 63, w = __builtin_amdgcn_readfirstlane(tid() >> 6), q = lane >> 4, c16 = lane & 15;
-  const int next = tl.layer + 1;
+// One Conv1d(64, 64, 3, dilation=dil, padding=dil) over the tile, src -> dst: this wave's 2 M-tiles
+// x 10 N-tiles, k-step outer (header).
+template <int EPI, bool EDGE>
+__device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int dil, Frags& F, bool has_next = true) {
+  const int lane = tid() & 63, w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB, q = lane >> 4,
+            c16 = lane & 15;
+  const int next = tl.layer + 1, mt = 2 * h;
+  asm volatile("" : "+s"(src), "+s"(dst));   // per-layer addresses: not hoisted out of a network's loop (spills)
   const BAddr ba(tl, src, dil);
-  int sa[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) sa[u] = (int)dst + tl.koff[2][u];
-  const int pos0 = tl.base + w * RW;
+  const int sa = (int)dst + (h ? tl.koff[2][1] : tl.koff[2][0]);     // slot 4h + q of row r0
+  const int pos0 = tl.base + (w % RB) * RW;
 
   // Idle waves of a short last tile: every row of this wave lies at position >= L + 2, beyond the
   // reach (d <= 2) of any row that matters, so it skips the layer (its dst rows are never read by
   // a stored output: positions L, L + 1 are re-zeroed by the wave that owns them, and the wrapped
   // taps of rows 0, 1 erode into the halo like any other edge).  Its SIMD partner wave then has the
   // MFMA pipe to itself.  It still fetches the next layer's operands and meets the barrier.
-  if (EDGE && __builtin_amdgcn_readfirstlane(pos0) >= tl.L + 2) {
+  if (EDGE && pos0 >= tl.L + 2) {
     if (has_next) load_frags(tl, next, F);
-#pragma unroll
-    for (int n = 0; n < NT; ++n) out[n] = 0.f;
     tl.layer += 1;
-    if (NM == 4) lds_barrier();
+    lds_barrier();
     return;
   }
 
-  // bias (+ identity), ReLU, zero rows outside [0, L), round to bf16, store the 8 channels of
-  // M-tiles 2u, 2u+1 as one 16-B slot
-  auto epilogue = [&](int n, int u, const f32x4 (&acc)[NM]) {
+  // bias (+ identity), ReLU, zero rows outside [0, L), round, store the 8 channels of M-tiles
+  // 2h, 2h+1 of N-tile n as one 16-B slot
+  auto epilogue = [&](int n, const f32x4& a0, const f32x4& a1) {
     const bool valid = !EDGE || in_range(pos0 + 16 * n + c16, tl.L);
-    f32x8 v = __builtin_shufflevector(acc[2 * u], acc[2 * u + 1], 0, 1, 2, 3, 4, 5, 6, 7);
-    V* p = (V*)(tl.lds + sa[u] + n * 16 * ROWB);
+    f32x8 v = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+    V* p = (V*)(tl.lds + sa + n * 16 * ROWB);
     if (EPI == RES_RELU) v += __builtin_convertvector(*p, f32x8);
 #if RDN_H16_F16 && RDN_H16_PKRELU
     // ReLU after the rounding, on packed f16 (4 v_pk_max_f16 instead of 8 v_max_f32; the rounding is
     // monotone, so max(f16(v), 0) = f16(max(v, 0)) up to the sign of a zero)
-    V h = __builtin_convertvector(v, V);
-    if (EPI != LINEAR) h = __builtin_elementwise_max(h, (V)((E)0));
-    if (EDGE && !valid) h = (V)((E)0);
-#if defined(RDN_ABLATE_NOSTORE)
-    if (h[0] == (E)1234.f)
+    V hv = __builtin_convertvector(v, V);
+    if (EPI != LINEAR) hv = __builtin_elementwise_max(hv, (V)((E)0));
+    if (EDGE && !valid) hv = (V)((E)0);
+#if defined(RDN_ABLATE_NOSTORE)            // diagnostic builds only (tools/ablate.py)
+    if (hv[0] == (E)1234.f)
 #endif
-    *p = h;
+    *p = hv;
 #else
     if (EPI != LINEAR) v = __builtin_elementwise_max(v, (f32x8)(0.f));
     if (EDGE && !valid) v = (f32x8)(0.f);
-#if defined(RDN_ABLATE_NOSTORE)            // diagnostic builds only (tools/ablate.py)
+#if defined(RDN_ABLATE_NOSTORE)
     if (v[0] == 123456.f)
 #endif
     *p = __builtin_convertvector(v, V);
 #endif
   };
 
-  f32x4 prev[NM];
-  constexpr int PF = RDN_H16_PF;       // B fragments in flight ahead of the k-step that computes
+  f32x4 acc[NT][2];
+  constexpr int PF = RDN_H16_PF;       // B fragments in flight ahead of the step that consumes them
+  constexpr int K = 6 * NT;            // steps (k-step s, N-tile n), k = s * NT + n
   V B[PF + 1];
 #pragma unroll
-  for (int k = 0; k < PF; ++k) B[k] = *(const V*)(tl.lds + ba.at(k / 6, k % 6));
+  for (int k = 0; k < PF; ++k) B[k] = *(const V*)(tl.lds + ba.at(k % NT, k / NT));
 #pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    f32x4 acc[NM];
+  for (int s = 0; s < 6; ++s) {
 #pragma unroll
-    for (int m = 0; m < NM; ++m) acc[m] = F.bias[m];
-    if (n == NT - 1 && has_next) {                            // last use of the bias in this layer
-#pragma unroll
-      for (int m = 0; m < 4; ++m) F.bias[m] = load_bias(tl, next, m, 16 * q);
-    }
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int k = 6 * n + s, kp = k + PF;
+    for (int n = 0; n < NT; ++n) {
+      const int k = s * NT + n, kp = k + PF;
 #if defined(RDN_ABLATE_NOLDS)
-      if (kp < 6 * NT) { B[kp % (PF + 1)] = B[(k + 1) % (PF + 1)]; asm volatile("" : "+v"(B[kp % (PF + 1)])); }
+      if (kp < K) { B[kp % (PF + 1)] = B[(k + 1) % (PF + 1)]; asm volatile("" : "+v"(B[kp % (PF + 1)])); }
 #else
-      if (kp < 6 * NT) B[kp % (PF + 1)] = *(const V*)(tl.lds + ba.at(kp / 6, kp % 6));
+      if (kp < K) B[kp % (PF + 1)] = *(const V*)(tl.lds + ba.at(kp % NT, kp / NT));
 #endif
       const V b = B[k % (PF + 1)];
 #pragma unroll
-      for (int m = 0; m < NM; ++m) {
+      for (int m = 0; m < 2; ++m) {
 #if defined(RDN_ABLATE_NOMFMA)
-        asm volatile("" : "+v"(acc[m]) : "v"(F.a[m][s]), "v"(b));
+        if (s == 0) acc[n][m] = F.bias[m];
+        asm volatile("" : "+v"(acc[n][m]) : "v"(F.a[m][s]), "v"(b));
 #else
-        acc[m] = mma(F.a[m][s], b, acc[m]);
+        acc[n][m] = mma(F.a[m][s], b, s == 0 ? F.bias[m] : acc[n][m]);
 #endif
       }
-#if defined(RDN_ABLATE_NOALOAD)
-      if (false) {
-#else
-      if (n == NT - 1 && has_next) {                          // last use of a[.][s] in this layer
-#endif
-#pragma unroll
-        for (int m = 0; m < 4; ++m) F.a[m][s] = load_frag(tl, next, m, s, 16 * lane);
-      }
-      if (NM == 4 && n > 0 && (s == 1 || s == 3)) epilogue(n - 1, s >> 1, prev);
+      if (s == 5 && n > 0) epilogue(n - 1, acc[n - 1][0], acc[n - 1][1]);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // head: M-row 0 holds f16/bf16(W), M-row 1 the rounding residue W - hi (pack.cpp
-    // pack_big_bf16): the two partial sums add in fp32, so the head's weights are exact to ~2^-22
-    // at no extra MFMA (the head's output feeds the RRCDNet cancellation x - (r + l)/2)
-    if (NM == 1) out[n] = acc[0][0] + acc[0][1];
+#if !defined(RDN_ABLATE_NOALOAD)
+    if (has_next) {                    // k-step s's fragments (and, after s = 0, the bias) are dead
 #pragma unroll
-    for (int m = 0; m < NM; ++m) prev[m] = acc[m];
+      for (int m = 0; m < 2; ++m) F.a[m][s] = load_frag(tl, next, mt + m, s, 16 * lane);
+      if (s == 0) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) F.bias[m] = load_bias(tl, next, mt + m, 16 * q);
+      }
+    }
+#endif
   }
-  if (NM == 4) {
-    epilogue(NT - 1, 0, prev);
-    epilogue(NT - 1, 1, prev);
-  }
+  epilogue(NT - 1, acc[NT - 1][0], acc[NT - 1][1]);
   tl.layer += 1;
 #if defined(RDN_ABLATE_NOBARRIER)
-  if (NM == 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #else
-  if (NM == 4) lds_barrier();
+  lds_barrier();
 #endif
 }
 
-template <int EPI, bool EDGE>
-__device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int dil, Frags& F, bool has_next = true) {
-  float unused[NT];
-  conv<EPI, 4, EDGE>(tl, src, dst, dil, F, has_next, unused);
-}
-
+// Conv1d(64, 1, 3) head, packed as a big layer whose M-tiles 0 and 2 both hold cout 0 in row 0 and
+// its weights' rounding residue in row 1 (pack.cpp pack_big_bf16: the two partial sums add in fp32,
+// so the head's weights are exact to ~2^-22 at no extra MFMA; the head feeds the RRCDNet
+// cancellation x - (r + l)/2).  Half h computes N-tiles h*HN .. h*HN + HN-1 of its row block from
+// M-tile 2h; out[j] = cout 0 of row head_row(j), in lanes 0..15.  No write, no barrier.
 template <bool EDGE>
-__device__ __forceinline__ void head(Tile& tl, uint32_t src, Frags& F, bool has_next, float (&out)[NT]) {
-  conv<LINEAR, 1, EDGE>(tl, src, src, 1, F, has_next, out);
+__device__ __forceinline__ void head(Tile& tl, uint32_t src, Frags& F, bool has_next, float (&out)[HN]) {
+  const int lane = tid() & 63, w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB, q = lane >> 4;
+  const int next = tl.layer + 1, mt = 2 * h;
+  const BAddr ba(tl, src, 1);
+  const int pos0 = tl.base + (w % RB) * RW + 16 * HN * h;
+  if (EDGE && pos0 >= tl.L + 2) {
+    if (has_next) load_frags(tl, next, F);
+#pragma unroll
+    for (int j = 0; j < HN; ++j) out[j] = 0.f;
+    tl.layer += 1;
+    return;
+  }
+  // N-tile h*HN + j: only (j = 0, t = 0) of half 0 and (j = HN-1, t = 2) of half 1 can leave the tile
+  auto addr = [&](int j, int s) {
+    const int t = s >> 1, u = s & 1;
+    const int plain = ba.m[s] + (h * HN + j) * 16 * ROWB;
+    if (j == 0 && t == 0) return h == 0 ? ba.first[u] : plain;
+    if (j == HN - 1 && t == 2) return h == MH - 1 ? ba.last[u] : plain;
+    return plain;
+  };
+  f32x4 acc[HN];
+  constexpr int PF = RDN_H16_PF, K = 6 * HN;
+  V B[PF + 1];
+#pragma unroll
+  for (int k = 0; k < PF; ++k) B[k] = *(const V*)(tl.lds + addr(k % HN, k / HN));
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+#pragma unroll
+    for (int j = 0; j < HN; ++j) {
+      const int k = s * HN + j, kp = k + PF;
+      if (kp < K) B[kp % (PF + 1)] = *(const V*)(tl.lds + addr(kp % HN, kp / HN));
+      acc[j] = mma(F.a[0][s], B[k % (PF + 1)], s == 0 ? F.bias[0] : acc[j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (has_next) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) F.a[m][s] = load_frag(tl, next, mt + m, s, 16 * lane);
+      if (s == 0) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) F.bias[m] = load_bias(tl, next, mt + m, 16 * q);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < HN; ++j) out[j] = acc[j][0] + acc[j][1];
+  tl.layer += 1;
 }
 
 __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const float* x, int L, int T, int tiles,
@@ -366,7 +400,7 @@ __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const 
   tl.wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)tl.big, 0, 0x7fffffff, 0x00020000);
   tl.layer = 0;
   const int t = tid(), q = (t & 63) >> 4;
-  tl.r0 = (t >> 6) * RW + (t & 15);
+  tl.r0 = ((t >> 6) % RB) * RW + (t & 15);
 #pragma unroll
   for (int d = -2; d <= 2; ++d)
 #pragma unroll
@@ -374,12 +408,16 @@ __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const 
   return tl;
 }
 
-__device__ __forceinline__ int head_row(int k) { return (tid() >> 6) * RW + 16 * k + (tid() & 15); }
+// tile row of head output j of this lane (lanes 0..15)
+__device__ __forceinline__ int head_row(int j) {
+  const int w = tid() >> 6;
+  return (w % RB) * RW + 16 * (HN * (w / RB) + j) + (tid() & 15);
+}
 
-__device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, const float (&v)[NT], int halo, int T) {
+__device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, const float (&v)[HN], int halo, int T) {
   if ((tid() & 63) >= 16) return;
 #pragma unroll
-  for (int k = 0; k < NT; ++k) {
+  for (int k = 0; k < HN; ++k) {
     const int j = head_row(k);
     const int p = tl.base + j;
     if (j >= halo && j < halo + T && p < tl.L) y[(size_t)n * tl.L + p] = v[k];

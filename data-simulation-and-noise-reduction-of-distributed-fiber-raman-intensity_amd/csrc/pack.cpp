@@ -232,9 +232,10 @@ static void pack_big_bf16(const Folded& f, uint8_t* dst, bool f16 = false) {
       for (int lane = 0; lane < 64; ++lane)
         for (int j = 0; j < 8; ++j) {
           const int t = s >> 1, u = s & 1;
-          const int co = 16 * m + (lane & 15), ci = h16_channel(4 * u + (lane >> 4), j);
+          // a head (cout = 1) sits in M-tiles 0 and 2 (rows 0 and 32: the M-tile of either
+          // output-channel half, fused16.hpp head); row 1 / 33 carries the residue of row 0's rounding
+          const int co = (f.cout == 1 && m == 2 ? 0 : 16 * m) + (lane & 15), ci = h16_channel(4 * u + (lane >> 4), j);
           double v = co < f.cout ? f.W(co, ci, t) : 0.0;
-          // a head (cout = 1): row 1 carries the residue of row 0's rounding (fused16.hip head)
           if (f.cout == 1 && co == 1) {
             const double w = f.W(0, ci, t);
             v = w - from16(f16 ? to_f16(w) : to_bf16(w), f16);
@@ -243,6 +244,7 @@ static void pack_big_bf16(const Folded& f, uint8_t* dst, bool f16 = false) {
         }
   float* bias = (float*)(dst + BIG_FRAG_BYTES_BF16);
   for (int c = 0; c < C; ++c) bias[c] = c < f.cout ? (float)f.b[c] : 0.f;
+  if (f.cout == 1) bias[32] = (float)f.b[0];        // the head's copy in M-tile 2
 }
 
 static void pack_big_f32(const Folded& f, uint8_t* dst) {
