@@ -11,51 +11,52 @@ namespace H16_NS {
 // whose rows every epilogue re-zeroes.  Interior tiles skip that per-row select.
 #define H16_BODY(name) template <bool EDGE> __device__ __forceinline__ void name##_body(Tile& tl, float* y, int n, int L, int T)
 
+// The bodies alternate the two operand buffers F0 / F1: a layer computes from one while the next
+// layer's operands stream into the other (fused16.hpp layer).
+
 // 1DCNN/train.py:71-82 — conv(1->64)+ReLU, 18 x [conv+ReLU], conv(64->1)
 H16_BODY(denoisecnn) {
   constexpr int H = fused_halo(DENOISECNN);
-  Frags F;
-  load_frags(tl, 0, F);
+  Frags F0, F1;
+  load_frags(tl, 0, F0);
   stem(tl, 0, BUF0);
   lds_barrier();
-  uint32_t cur = BUF0, nxt = BUF1;
-  for (int i = 0; i < 18; ++i) {
-    layer<RELU, EDGE>(tl, cur, nxt, 1, F);
-    const uint32_t t = cur; cur = nxt; nxt = t;
+  for (int i = 0; i < 9; ++i) {
+    layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F0, F1);
+    layer<RELU, EDGE>(tl, BUF1, BUF0, 1, F1, F0);
   }
   float o[HN];
-  head<EDGE>(tl, cur, F, false, o);
+  head<EDGE>(tl, BUF0, F0, F1, false, o);
   store_out(tl, y, n, o, H, T);
 }
 
 // RRCDNet/train.py:77-98 — right (BN, d=1) and left (dilated) branches, y = x - (r + l) / 2
 H16_BODY(rrcdnet) {
   constexpr int H = fused_halo(RRCDNET);
-  Frags F;
-  load_frags(tl, 0, F);
+  Frags F0, F1;
+  load_frags(tl, 0, F0);
   // right_net: conv+BN+ReLU, 15 x [conv+BN+ReLU], conv(64->1)
   stem(tl, 0, BUF0);
   lds_barrier();
-  uint32_t cur = BUF0, nxt = BUF1;
-  for (int i = 0; i < 15; ++i) {
-    layer<RELU, EDGE>(tl, cur, nxt, 1, F);
-    const uint32_t t = cur; cur = nxt; nxt = t;
+  for (int i = 0; i < 7; ++i) {
+    layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F0, F1);
+    layer<RELU, EDGE>(tl, BUF1, BUF0, 1, F1, F0);
   }
+  layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F0, F1);
   {
     float r[HN];
-    head<EDGE>(tl, cur, F, true, r);
+    head<EDGE>(tl, BUF1, F1, F0, true, r);
     store_out(tl, y, n, r, H, T);   // parked in the output (re-read below): no VGPRs held across the left branch
   }
   // left_net: conv+BN+ReLU, 7 x [conv d2 + ReLU], conv+BN+ReLU, 6 x [conv d2 + ReLU], conv(64->1)
-  stem(tl, 1, nxt);              // the head above reads `cur` only
+  stem(tl, 1, BUF0);             // the head above reads BUF1 only
   lds_barrier();
-  { const uint32_t t = cur; cur = nxt; nxt = t; }
-  for (int i = 0; i < 14; ++i) {
-    layer<RELU, EDGE>(tl, cur, nxt, i == 7 ? 1 : 2, F);
-    const uint32_t t = cur; cur = nxt; nxt = t;
+  for (int i = 0; i < 7; ++i) {
+    layer<RELU, EDGE>(tl, BUF0, BUF1, 2, F0, F1);
+    layer<RELU, EDGE>(tl, BUF1, BUF0, 2 * i + 1 == 7 ? 1 : 2, F1, F0);
   }
   float l[HN];
-  head<EDGE>(tl, cur, F, false, l);
+  head<EDGE>(tl, BUF0, F0, F1, false, l);
   // y = x - (right + left) / 2 on this tile's output rows (the lanes that stored r re-read it)
   if ((tid() & 63) < 16) {
 #pragma unroll
@@ -73,36 +74,36 @@ H16_BODY(rrcdnet) {
 // DSDN/train.py:120-126 — relu(relu(stem)), relu(conv1), relu(conv2), 15 ResNet blocks, conv_out
 H16_BODY(dsdn) {
   constexpr int H = fused_halo(DSDN);
-  Frags F;
-  load_frags(tl, 0, F);
+  Frags F0, F1;
+  load_frags(tl, 0, F0);
   stem(tl, 0, BUF0);
   lds_barrier();
-  layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F);           // conv1
-  layer<RELU, EDGE>(tl, BUF1, BUF0, 1, F);           // conv2
+  layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F0, F1);           // conv1
+  layer<RELU, EDGE>(tl, BUF1, BUF0, 1, F1, F0);           // conv2
   for (int b = 0; b < 15; ++b) {               // x in BUF0 is the block identity
-    layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F);         // relu(bn1(conv1 x))
-    layer<RES_RELU, EDGE>(tl, BUF1, BUF0, 1, F);     // relu(bn2(conv2 .) + x), written over x in place
+    layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F0, F1);         // relu(bn1(conv1 x))
+    layer<RES_RELU, EDGE>(tl, BUF1, BUF0, 1, F1, F0);     // relu(bn2(conv2 .) + x), written over x in place
   }
   float o[HN];
-  head<EDGE>(tl, BUF0, F, false, o);
+  head<EDGE>(tl, BUF0, F0, F1, false, o);
   store_out(tl, y, n, o, H, T);
 }
 
 // PIDN/train.py:101-106 — h = relu(stem x); 15 x [conv+BN+ReLU, conv+BN]; sigmoid(conv_out(y + h))
 H16_BODY(pidn) {
   constexpr int H = fused_halo(PIDN);
-  Frags F;
-  load_frags(tl, 0, F);
+  Frags F0, F1;
+  load_frags(tl, 0, F0);
   stem(tl, 0, BUF0);
   lds_barrier();
   for (int b = 0; b < 15; ++b) {
-    layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F);
-    layer<LINEAR, EDGE>(tl, BUF1, BUF0, 1, F);
+    layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F0, F1);
+    layer<LINEAR, EDGE>(tl, BUF1, BUF0, 1, F1, F0);
   }
   stem<true>(tl, 0, BUF0);       // + identity (the stem output), recomputed in fp32 from x
   lds_barrier();
   float o[HN];
-  head<EDGE>(tl, BUF0, F, false, o);
+  head<EDGE>(tl, BUF0, F0, F1, false, o);
 #pragma unroll
   for (int k = 0; k < HN; ++k) o[k] = 1.0f / (1.0f + expf(-o[k]));
   store_out(tl, y, n, o, H, T);

@@ -20,12 +20,13 @@
 // channels of the same rows.  The split halves the weights a wave holds (12 A-fragments, 12 KB per
 // layer, loaded from L2/L1 by every wave: 96 KB per CU per layer instead of 192 KB -- the vector
 // memory path, not the MFMA, bounded the all-channels-per-wave layout) at the price of twice the
-// LDS B reads (480 KB per CU per layer at 256 B/clk: half the MFMA time).  The k-steps are the
-// OUTER loop: fragment (m, s) is dead after k-step s, so the next layer's copy is fetched right
-// there and the weight traffic spreads evenly over the layer (no burst at its end), while the
-// NT x 2 accumulators (80 VGPRs) stay live.  Accumulators start at the folded bias; ReLU
-// (+ residual) and the rounding run in an epilogue that trails the last k-step's MFMAs by one
-// N-tile, one ds_write_b128 per N-tile.  One LDS barrier per layer.
+// LDS B reads (480 KB per CU per layer at 256 B/clk: half the MFMA time).  The layer's
+// operands are double-buffered (two Frags, the network bodies alternate them): the next layer's
+// 14 loads are spread one per 4 steps over the layer, so the vector-memory traffic of the CU's
+// 8 waves is smooth instead of a burst at the layer's end.  N-tiles are the outer loop, so each
+// N-tile's ReLU (+ residual), rounding and ds_write_b128 run one N-tile behind the MFMAs, spread
+// over the layer (a k-step-outer loop bunched all of them, issue-bound, into its last sixth).
+// Accumulators start at the folded bias.  One LDS barrier per layer.
 //
 // Channel order inside an LDS row (= K order of the packed A-fragments, csrc/pack.cpp): 16-B slot
 // g = 4u + q holds channels h16_channel(g, j) = 32u + 4q + (j & 3) + 16 (j >> 2), j = 0..7 — the
@@ -71,7 +72,7 @@ constexpr uint32_t BUF0 = 0, BUF1 = BUF_BYTES;
 constexpr int LAYER_BYTES = H16_LAYER_BYTES;          // [m 4][k-step 6][lane 64][8 x 16 bit] ... bias[64] f32
 constexpr int BIAS_OFF = H16_BIAS_OFF;
 #ifndef RDN_H16_PF
-#define RDN_H16_PF 5
+#define RDN_H16_PF 3
 #endif
 #ifndef RDN_H16_PKRELU
 #define RDN_H16_PKRELU 1
@@ -231,9 +232,10 @@ struct BAddr {
 };
 
 // One Conv1d(64, 64, 3, dilation=dil, padding=dil) over the tile, src -> dst: this wave's 2 M-tiles
-// x 10 N-tiles, k-step outer (header).
+// x 10 N-tiles from the operands in F, while the next layer's operands stream into G (header).
 template <int EPI, bool EDGE>
-__device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int dil, Frags& F, bool has_next = true) {
+__device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int dil, const Frags& F, Frags& G,
+                                      bool has_next = true) {
   const int lane = tid() & 63, w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB, q = lane >> 4,
             c16 = lane & 15;
   const int next = tl.layer + 1, mt = 2 * h;
@@ -248,7 +250,7 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   // taps of rows 0, 1 erode into the halo like any other edge).  Its SIMD partner wave then has the
   // MFMA pipe to itself.  It still fetches the next layer's operands and meets the barrier.
   if (EDGE && pos0 >= tl.L + 2) {
-    if (has_next) load_frags(tl, next, F);
+    if (has_next) load_frags(tl, next, G);
     tl.layer += 1;
     lds_barrier();
     return;
@@ -281,47 +283,49 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
 #endif
   };
 
-  f32x4 acc[NT][2];
+  f32x4 prev[2];
   constexpr int PF = RDN_H16_PF;       // B fragments in flight ahead of the step that consumes them
-  constexpr int K = 6 * NT;            // steps (k-step s, N-tile n), k = s * NT + n
+  constexpr int K = 6 * NT;            // steps (N-tile n, k-step s), k = 6n + s
   V B[PF + 1];
 #pragma unroll
-  for (int k = 0; k < PF; ++k) B[k] = *(const V*)(tl.lds + ba.at(k % NT, k / NT));
+  for (int k = 0; k < PF; ++k) B[k] = *(const V*)(tl.lds + ba.at(k / 6, k % 6));
 #pragma unroll
-  for (int s = 0; s < 6; ++s) {
+  for (int n = 0; n < NT; ++n) {
+    f32x4 acc[2];
 #pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const int k = s * NT + n, kp = k + PF;
+    for (int s = 0; s < 6; ++s) {
+      const int k = 6 * n + s, kp = k + PF;
 #if defined(RDN_ABLATE_NOLDS)
       if (kp < K) { B[kp % (PF + 1)] = B[(k + 1) % (PF + 1)]; asm volatile("" : "+v"(B[kp % (PF + 1)])); }
 #else
-      if (kp < K) B[kp % (PF + 1)] = *(const V*)(tl.lds + ba.at(kp % NT, kp / NT));
+      if (kp < K) B[kp % (PF + 1)] = *(const V*)(tl.lds + ba.at(kp / 6, kp % 6));
 #endif
       const V b = B[k % (PF + 1)];
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
 #if defined(RDN_ABLATE_NOMFMA)
-        if (s == 0) acc[n][m] = F.bias[m];
-        asm volatile("" : "+v"(acc[n][m]) : "v"(F.a[m][s]), "v"(b));
+        if (s == 0) acc[m] = F.bias[m];
+        asm volatile("" : "+v"(acc[m]) : "v"(F.a[m][s]), "v"(b));
 #else
-        acc[n][m] = mma(F.a[m][s], b, s == 0 ? F.bias[m] : acc[n][m]);
+        acc[m] = mma(F.a[m][s], b, s == 0 ? F.bias[m] : acc[m]);
 #endif
       }
-      if (s == 5 && n > 0) epilogue(n - 1, acc[n - 1][0], acc[n - 1][1]);
+      if (n > 0 && s == 1) epilogue(n - 1, prev[0], prev[1]);
+#if !defined(RDN_ABLATE_NOALOAD)
+      // the next layer's 12 fragments + 2 bias vectors, one buffer load every 4th step: the vector
+      // memory traffic of the CU's 8 waves spreads over the whole layer
+      if (has_next && k % 4 == 0 && k / 4 < 14) {
+        const int i = k / 4;
+        if (i < 12) G.a[i / 6][i % 6] = load_frag(tl, next, mt + i / 6, i % 6, 16 * lane);
+        else G.bias[i - 12] = load_bias(tl, next, mt + i - 12, 16 * q);
+      }
+#endif
       __builtin_amdgcn_sched_barrier(0);
     }
-#if !defined(RDN_ABLATE_NOALOAD)
-    if (has_next) {                    // k-step s's fragments (and, after s = 0, the bias) are dead
-#pragma unroll
-      for (int m = 0; m < 2; ++m) F.a[m][s] = load_frag(tl, next, mt + m, s, 16 * lane);
-      if (s == 0) {
-#pragma unroll
-        for (int m = 0; m < 2; ++m) F.bias[m] = load_bias(tl, next, mt + m, 16 * q);
-      }
-    }
-#endif
+    prev[0] = acc[0];
+    prev[1] = acc[1];
   }
-  epilogue(NT - 1, acc[NT - 1][0], acc[NT - 1][1]);
+  epilogue(NT - 1, prev[0], prev[1]);
   tl.layer += 1;
 #if defined(RDN_ABLATE_NOBARRIER)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -334,15 +338,17 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
 // its weights' rounding residue in row 1 (pack.cpp pack_big_bf16: the two partial sums add in fp32,
 // so the head's weights are exact to ~2^-22 at no extra MFMA; the head feeds the RRCDNet
 // cancellation x - (r + l)/2).  Half h computes N-tiles h*HN .. h*HN + HN-1 of its row block from
-// M-tile 2h; out[j] = cout 0 of row head_row(j), in lanes 0..15.  No write, no barrier.
+// M-tile 2h (F.a[0]); out[j] = cout 0 of row head_row(j), in lanes 0..15.  No write, no barrier;
+// the next layer's operands stream into G.
 template <bool EDGE>
-__device__ __forceinline__ void head(Tile& tl, uint32_t src, Frags& F, bool has_next, float (&out)[HN]) {
+__device__ __forceinline__ void head(Tile& tl, uint32_t src, const Frags& F, Frags& G, bool has_next,
+                                     float (&out)[HN]) {
   const int lane = tid() & 63, w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB, q = lane >> 4;
   const int next = tl.layer + 1, mt = 2 * h;
   const BAddr ba(tl, src, 1);
   const int pos0 = tl.base + (w % RB) * RW + 16 * HN * h;
   if (EDGE && pos0 >= tl.L + 2) {
-    if (has_next) load_frags(tl, next, F);
+    if (has_next) load_frags(tl, next, G);
 #pragma unroll
     for (int j = 0; j < HN; ++j) out[j] = 0.f;
     tl.layer += 1;
@@ -356,31 +362,27 @@ __device__ __forceinline__ void head(Tile& tl, uint32_t src, Frags& F, bool has_
     if (j == HN - 1 && t == 2) return h == MH - 1 ? ba.last[u] : plain;
     return plain;
   };
-  f32x4 acc[HN];
   constexpr int PF = RDN_H16_PF, K = 6 * HN;
   V B[PF + 1];
 #pragma unroll
-  for (int k = 0; k < PF; ++k) B[k] = *(const V*)(tl.lds + addr(k % HN, k / HN));
+  for (int k = 0; k < PF; ++k) B[k] = *(const V*)(tl.lds + addr(k / 6, k % 6));
 #pragma unroll
-  for (int s = 0; s < 6; ++s) {
+  for (int j = 0; j < HN; ++j) {
+    f32x4 acc;
 #pragma unroll
-    for (int j = 0; j < HN; ++j) {
-      const int k = s * HN + j, kp = k + PF;
-      if (kp < K) B[kp % (PF + 1)] = *(const V*)(tl.lds + addr(kp % HN, kp / HN));
-      acc[j] = mma(F.a[0][s], B[k % (PF + 1)], s == 0 ? F.bias[0] : acc[j]);
+    for (int s = 0; s < 6; ++s) {
+      const int k = 6 * j + s, kp = k + PF;
+      if (kp < K) B[kp % (PF + 1)] = *(const V*)(tl.lds + addr(kp / 6, kp % 6));
+      acc = mma(F.a[0][s], B[k % (PF + 1)], s == 0 ? F.bias[0] : acc);
+      if (has_next && k % 2 == 0 && k / 2 < 14) {
+        const int i = k / 2;
+        if (i < 12) G.a[i / 6][i % 6] = load_frag(tl, next, mt + i / 6, i % 6, 16 * lane);
+        else G.bias[i - 12] = load_bias(tl, next, mt + i - 12, 16 * q);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (has_next) {
-#pragma unroll
-      for (int m = 0; m < 2; ++m) F.a[m][s] = load_frag(tl, next, mt + m, s, 16 * lane);
-      if (s == 0) {
-#pragma unroll
-        for (int m = 0; m < 2; ++m) F.bias[m] = load_bias(tl, next, mt + m, 16 * q);
-      }
-    }
+    out[j] = acc[0] + acc[1];
   }
-#pragma unroll
-  for (int j = 0; j < HN; ++j) out[j] = acc[j][0] + acc[j][1];
   tl.layer += 1;
 }
 

@@ -193,15 +193,17 @@ __device__ __forceinline__ void rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   using HO = HeadOut<MODE_H8, NBK>;
   int n16;
   h16x::Tile t16 = h16x::make_tile(tl.lds, blob, x, L, T, tiles, H, n16);
-  h16x::Frags F;
-  h16x::load_frags(t16, 0, F);
+  static_assert(PP % 2 == 1, "the ping-pong run ends on F0 -> BUF1");
+  h16x::Frags F0, F1;            // alternating operand buffers (fused16.hpp layer)
+  h16x::load_frags(t16, 0, F0);
   h16x::stem(t16, 0, h16x::BUF0);
   h16x::lds_barrier();
-  uint32_t cur = h16x::BUF0, nxt = h16x::BUF1;
-  for (int i = 0; i < PP; ++i) {
-    h16x::layer<h16x::RELU, EDGE>(t16, cur, nxt, 1, F, i + 1 < PP);
-    const uint32_t s = cur; cur = nxt; nxt = s;
+  for (int i = 0; i < PP / 2; ++i) {
+    h16x::layer<h16x::RELU, EDGE>(t16, h16x::BUF0, h16x::BUF1, 1, F0, F1);
+    h16x::layer<h16x::RELU, EDGE>(t16, h16x::BUF1, h16x::BUF0, 1, F1, F0);
   }
+  h16x::layer<h16x::RELU, EDGE>(t16, h16x::BUF0, h16x::BUF1, 1, F0, F1, false);
+  uint32_t cur = h16x::BUF1;
   f32x4 id[16 * NBK / 4];
   LayerA<MODE_H8> a;
   tl.layer = PP;
@@ -213,15 +215,16 @@ __device__ __forceinline__ void rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   head<MODE_H8, NBK>(tl, 2, r);
   // left branch: layers 15-27 ping-pong, 28 in place (it writes the e4m3 lo plane the head reads)
   t16.layer = 15;
-  h16x::load_frags(t16, 15, F);
+  h16x::load_frags(t16, 15, F0);
   __syncthreads();               // the left stem overwrites the rows the right head just read
   h16x::stem(t16, 1, h16x::BUF0);
   h16x::lds_barrier();
-  cur = h16x::BUF0; nxt = h16x::BUF1;
-  for (int i = 0; i < 13; ++i) {
-    h16x::layer<h16x::RELU, EDGE>(t16, cur, nxt, i == 7 ? 1 : 2, F, i + 1 < 13);
-    const uint32_t s = cur; cur = nxt; nxt = s;
+  for (int i = 0; i < 6; ++i) {  // left layers 15-26 (the one at 22 with d = 1), then 27
+    h16x::layer<h16x::RELU, EDGE>(t16, h16x::BUF0, h16x::BUF1, 2, F0, F1);
+    h16x::layer<h16x::RELU, EDGE>(t16, h16x::BUF1, h16x::BUF0, 2 * i + 1 == 7 ? 1 : 2, F1, F0);
   }
+  h16x::layer<h16x::RELU, EDGE>(t16, h16x::BUF0, h16x::BUF1, 2, F0, F1, false);
+  cur = h16x::BUF1;
   tl.layer = 28;
   load_layer_a<MODE_H8>(tl, 28, a);
   pingpong_to_tile(tl.lds, cur);

@@ -25,7 +25,7 @@ VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "hibase0": "-DRDN_IP_HIBASE=0", "dsdn3": "-DRDN_DSDN_NBK=3", "comp0": "-DRDN_F32_COMP=0",
             "chunk1": "-DRDN_F32_CHUNK=1", "chunk3": "-DRDN_F32_CHUNK=3", "chunk4": "-DRDN_F32_CHUNK=4",
             "h16f16": "-DRDN_H16_F16=1", "h8plain": "-DRDN_ABLATE_H8_PLAIN", "nohead": "-DRDN_ABLATE_NOHEAD",
-            "mixold": "-DRDN_F16MIX_HYBRID=0", "pkrelu0": "-DRDN_H16_PKRELU=0", "pf4": "-DRDN_H16_PF=4", "pf7": "-DRDN_H16_PF=7"}
+            "mixold": "-DRDN_F16MIX_HYBRID=0", "pkrelu0": "-DRDN_H16_PKRELU=0", "pf2": "-DRDN_H16_PF=2", "pf4": "-DRDN_H16_PF=4", "pf5": "-DRDN_H16_PF=5"}
 
 
 def build():
