@@ -22,7 +22,7 @@
 // memory path, not the MFMA, bounded the all-channels-per-wave layout) at the price of twice the
 // LDS B reads (480 KB per CU per layer at 256 B/clk: half the MFMA time).  The layer's
 // operands are double-buffered (two Frags, the network bodies alternate them): the next layer's
-// 14 loads are spread one per 4 steps over the layer, so the vector-memory traffic of the CU's
+// 14 loads are spread one per 4 steps, so the vector-memory traffic of the CU's
 // 8 waves is smooth instead of a burst at the layer's end.  N-tiles are the outer loop, so each
 // N-tile's ReLU (+ residual), rounding and ds_write_b128 run one N-tile behind the MFMAs, spread
 // over the layer (a k-step-outer loop bunched all of them, issue-bound, into its last sixth).
@@ -73,6 +73,9 @@ constexpr int LAYER_BYTES = H16_LAYER_BYTES;          // [m 4][k-step 6][lane 64
 constexpr int BIAS_OFF = H16_BIAS_OFF;
 #ifndef RDN_H16_PF
 #define RDN_H16_PF 3
+#endif
+#ifndef RDN_H16_LDSTEP
+#define RDN_H16_LDSTEP 4
 #endif
 #ifndef RDN_H16_PKRELU
 #define RDN_H16_PKRELU 1
@@ -312,12 +315,19 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
       }
       if (n > 0 && s == 1) epilogue(n - 1, prev[0], prev[1]);
 #if !defined(RDN_ABLATE_NOALOAD)
-      // the next layer's 12 fragments + 2 bias vectors, one buffer load every 4th step: the vector
-      // memory traffic of the CU's 8 waves spreads over the whole layer
-      if (has_next && k % 4 == 0 && k / 4 < 14) {
-        const int i = k / 4;
+      // the next layer's 12 fragments + 2 bias vectors, one buffer load every LDSTEP-th step: the
+      // vector-memory traffic of the CU's 8 waves spreads over the layer (denser is slower: 2 steps
+      // -2 %, 3 steps -0.5 % against 4)
+      constexpr int LDSTEP = RDN_H16_LDSTEP;
+      if (has_next && k % LDSTEP == 0 && k / LDSTEP < 14) {
+        const int i = k / LDSTEP;
+#if defined(RDN_ABLATE_ALOAD_LDS)          // diagnostic: the same VGPR traffic from LDS instead of L1/L2
+        if (i < 12) G.a[i / 6][i % 6] = *(const V*)(tl.lds + 16 * lane + 1024 * i);
+        else G.bias[i - 12] = *(const f32x4*)(tl.lds + 16 * lane + 1024 * i);
+#else
         if (i < 12) G.a[i / 6][i % 6] = load_frag(tl, next, mt + i / 6, i % 6, 16 * lane);
         else G.bias[i - 12] = load_bias(tl, next, mt + i - 12, 16 * q);
+#endif
       }
 #endif
       __builtin_amdgcn_sched_barrier(0);

@@ -25,7 +25,7 @@ VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "hibase0": "-DRDN_IP_HIBASE=0", "dsdn3": "-DRDN_DSDN_NBK=3", "comp0": "-DRDN_F32_COMP=0",
             "chunk1": "-DRDN_F32_CHUNK=1", "chunk3": "-DRDN_F32_CHUNK=3", "chunk4": "-DRDN_F32_CHUNK=4",
             "h16f16": "-DRDN_H16_F16=1", "h8plain": "-DRDN_ABLATE_H8_PLAIN", "nohead": "-DRDN_ABLATE_NOHEAD",
-            "mixold": "-DRDN_F16MIX_HYBRID=0", "pkrelu0": "-DRDN_H16_PKRELU=0", "pf2": "-DRDN_H16_PF=2", "pf4": "-DRDN_H16_PF=4", "pf5": "-DRDN_H16_PF=5"}
+            "mixold": "-DRDN_F16MIX_HYBRID=0", "pkrelu0": "-DRDN_H16_PKRELU=0", "ld2": "-DRDN_H16_LDSTEP=2", "ld4": "-DRDN_H16_LDSTEP=4", "alds": "-DRDN_ABLATE_ALOAD_LDS"}
 
 
 def build():
@@ -83,8 +83,9 @@ def run():
     aid = engine._arch(arch)
     model = R.MODELS[arch]()
     libs = {}
+    only = os.environ.get("ABLATE_ONLY", "").split(",") if os.environ.get("ABLATE_ONLY") else None
     for name in VARIANTS:
-        if not os.path.exists(os.path.join(OUT, f"lib_{name}.so")):
+        if not os.path.exists(os.path.join(OUT, f"lib_{name}.so")) or (only and name not in only):
             continue
         lib = ctypes.CDLL(os.path.join(OUT, f"lib_{name}.so"))
         for fn, (args, res) in _lib._SIGNATURES.items():

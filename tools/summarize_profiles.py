@@ -16,7 +16,7 @@ import os
 import shutil
 import sys
 
-KERNELS = {"f16": "rdn::ip::rrcdnet<3, 3>", "f16-plain": "rdn::h16f::rrcdnet", "f16f8": "rdn::ip::rrcdnet<3, 0>",
+KERNELS = {"f16": "rdn::ip::rrcdnet_hybrid<3>", "f16-plain": "rdn::h16f::rrcdnet", "f16f8": "rdn::ip::rrcdnet<3, 0>",
            "bf16x3": "rdn::ip::rrcdnet<2, 0>", "bf16-unsafe": "rdn::h16::rrcdnet"}
 BATCH = 8192          # bench.py default --batch (the PMC passes run the default batch)
 
