@@ -237,16 +237,33 @@ def main():
     ap.add_argument("--no-batch1", action="store_true", help="skip the batch-1 evaluate-loop latency")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip timing the simulate -> forward -> metrics pipeline (SURVEY.md §8d configs 3-4)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL over xGMI, one rank per GPU); gloo rehearses the N>1 path with ranks "
+                         "sharing the visible GPUs (collectives staged through host memory)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gloo = world > 1 and args.dist_backend == "gloo"
+    if gloo:
+        local = local % torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+
+    def all_reduce(t, op=dist.ReduceOp.SUM):
+        if gloo:                                  # gloo reduces host tensors
+            h = t.cpu()
+            dist.all_reduce(h, op=op)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op)
 
     import raman_mi355x as R
     from raman_mi355x import engine
@@ -284,7 +301,7 @@ def main():
     kernel_ms = ev0.elapsed_time(ev1) / args.steps      # one fused kernel launch per step
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
     # the timed launches ran unchecked (check=False); a failed CBAM hand-off would show as NaN here
@@ -293,7 +310,7 @@ def main():
     # evaluation metrics of the last step, all-reduced across ranks (RCCL over xGMI) — untimed
     _, sums = engine.metrics(y.view(B, L), clean)
     if world > 1:
-        dist.all_reduce(sums)
+        all_reduce(sums)
     sums = sums.cpu().tolist()
 
     variants = {}
@@ -331,7 +348,7 @@ def main():
             "config": {"workload": f"{args.arch} {args.dtype} fused forward, on-device simulator inputs "
                                    "(BASELINE.json configs[2])", "engine_dtype_code": code,
                        "arch": args.arch, "signal_length": L, "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", **({"dist_backend": "gloo (rehearsal)"} if gloo else {})},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": tps * B if tps else None,
                          "traffic_source": tsrc, "algorithmic_bytes": 8 * L * B,
