@@ -147,6 +147,10 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
   if (!packed || !x || !y) return fail(RDN_EINVAL, "rdn_forward: null pointer");
   if (n < 0 || L < 1 || L > 0x7fffffff) return fail(RDN_EINVAL, "rdn_forward: need n >= 0 and 1 <= L < 2^31");
   if (n == 0) return RDN_OK;
+  {  // tiles re-read their input halos while other tiles' outputs (and parked head rows) land in y
+    const uintptr_t xb = (uintptr_t)x, yb = (uintptr_t)y, bytes = (uintptr_t)(n * L) * sizeof(float);
+    if (xb < yb + bytes && yb < xb + bytes) return fail(RDN_EINVAL, "rdn_forward: x and y overlap");
+  }
   const hipStream_t s = (hipStream_t)stream;
   const uint8_t* blob = (const uint8_t*)packed;
   if (is_cbam(arch)) {

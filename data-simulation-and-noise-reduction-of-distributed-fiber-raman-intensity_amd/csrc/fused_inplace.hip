@@ -22,6 +22,23 @@ namespace ip {
   template <int MODE, bool EDGE, int NBK, int TAIL> \
   __device__ __forceinline__ void name##_body(Tile& tl, float* y, int n, int L, int T)
 
+// RRCDNet's right-branch head outputs are parked in y (as fp32) over the left branch in the
+// vectorized-head modes, whose 5 double rows per lane would otherwise hold 10 VGPRs through it
+// (the f16f8 kernel spilled); the exact-fp32 and split modes keep their 2 doubles in registers.
+// The rounding of r to fp32 is 2^-24 relative, far below those modes' operand error.
+template <int MODE, int NBK>
+__device__ __forceinline__ void park_rows(const Tile& tl, float* y, int n, const double (&r)[HeadOut<MODE, NBK>::ROWS],
+                                          int H, int T) {
+  float o[HeadOut<MODE, NBK>::ROWS];
+  round_rows(r, o);
+  store_out<MODE, NBK>(tl, y, n, o, H, T);
+}
+template <int MODE, int NBK>
+__device__ __forceinline__ double parked_row(const Tile& tl, const float* y, int n, int k, int H, int T) {
+  const int j = HeadOut<MODE, NBK>::row(k), p = tl.base + j;
+  return HeadOut<MODE, NBK>::writer() && j >= H && j < H + T && p < tl.L ? (double)y[(size_t)n * tl.L + p] : 0.0;
+}
+
 // 128-row blocks per tile: 640-row tiles (the whole LDS, no guard rows) everywhere except DSDN,
 // whose ResidualBlock identity lives in VGPRs (20 vs 16 f32x4 per lane at 640 rows: spills).
 template <int ARCH> struct NetGeo { static constexpr int NBK = 5; };
@@ -70,8 +87,10 @@ IP_BODY(rrcdnet) {
     for (int i = 0; i < TAIL; ++i) conv<MODE, RELU, G::S, EDGE, NBK, true, true, true>(tl, 1, id, a, i + 1 < TAIL);
     load_layer_a<MODE>(tl, tl.layer, a);                // the left branch's first layer (f16 + e4m3)
   }
-  double r[HeadOut<MODE, NBK>::ROWS];
+  using HO = HeadOut<MODE, NBK>;
+  double r[HO::ROWS];
   head<MODE, NBK>(tl, 2, r);
+  if constexpr (HO::VEC) park_rows<MODE, NBK>(tl, y, n, r, H, T);
   __syncthreads();               // the left stem overwrites the rows the right head just read
   stem<MODE, false, NBK>(tl, 1);
   __syncthreads();
@@ -82,14 +101,15 @@ IP_BODY(rrcdnet) {
     for (int i = 0; i < 13; ++i) conv<MODE, RELU, G::S, EDGE, NBK, false, false, false>(tl, i == 7 ? 1 : 2, id, a, true);
     conv<MODE, RELU, G::S, EDGE, NBK, false, true, false>(tl, 2, id, a, false);
   }
-  double l[HeadOut<MODE, NBK>::ROWS];
+  double l[HO::ROWS];
   head<MODE, NBK>(tl, 3, l);
-  float o[HeadOut<MODE, NBK>::ROWS];
+  float o[HO::ROWS];
 #pragma unroll
-  for (int k = 0; k < HeadOut<MODE, NBK>::ROWS; ++k) {      // x - (r + l)/2 from the unrounded heads, one rounding
-    const int p = tl.base + HeadOut<MODE, NBK>::row(k);
+  for (int k = 0; k < HO::ROWS; ++k) {      // x - (r + l)/2 from the unrounded heads, one rounding
+    const int p = tl.base + HO::row(k);
     const float xv = in_range(p, L) ? tl.x[p] : 0.f;
-    o[k] = (float)((double)xv - (r[k] + l[k]) * 0.5);
+    const double rv = HO::VEC ? parked_row<MODE, NBK>(tl, y, n, k, H, T) : r[k];
+    o[k] = (float)((double)xv - (rv + l[k]) * 0.5);
   }
   store_out<MODE, NBK>(tl, y, n, o, H, T);
 }
@@ -213,6 +233,7 @@ __device__ __forceinline__ void rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   for (int i = 0; i < TAIL; ++i) conv<MODE_H8, RELU, 1, EDGE, NBK, true, true, true>(tl, 1, id, a, i + 1 < TAIL);
   double r[HO::ROWS];
   head<MODE_H8, NBK>(tl, 2, r);
+  park_rows<MODE_H8, NBK>(tl, y, n, r, H, T);
   // left branch: layers 15-27 ping-pong, 28 in place (it writes the e4m3 lo plane the head reads)
   t16.layer = 15;
   h16x::load_frags(t16, 15, F0);
@@ -236,7 +257,7 @@ __device__ __forceinline__ void rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   for (int k = 0; k < HO::ROWS; ++k) {      // x - (r + l)/2 from the unrounded heads, one rounding
     const int p = tl.base + HO::row(k);
     const float xv = in_range(p, L) ? tl.x[p] : 0.f;
-    o[k] = (float)((double)xv - (r[k] + l[k]) * 0.5);
+    o[k] = (float)((double)xv - (parked_row<MODE_H8, NBK>(tl, y, n, k, H, T) + l[k]) * 0.5);
   }
   store_out<MODE_H8, NBK>(tl, y, n, o, H, T);
 }

@@ -110,7 +110,8 @@ int rdn_get_correction_mask(int arch, int dtype, const void* host_blob, size_t b
 int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes);
 
 /* y[n][L] = Model(x[n][L]) on the device.  x, y: fp32 device pointers (the (N,1,L) tensor is
- * (N,L) contiguous); packed: device copy of the rdn_pack blob; stream: hipStream_t or NULL. */
+ * (N,L) contiguous) that must not overlap (RDN_EINVAL: tiles re-read input halos while outputs are
+ * written); packed: device copy of the rdn_pack blob; stream: hipStream_t or NULL. */
 int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* y, int64_t n, int64_t L,
                 void* workspace, size_t workspace_bytes, void* stream);
 

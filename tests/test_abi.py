@@ -80,6 +80,11 @@ def test_errors_are_reported_not_raised(lib):
         engine.pack("DenoiseCNN", sd, "fp32", "cpu")
     with pytest.raises(KeyError):
         engine.pack("DenoiseCNN", {}, "fp32", "cpu")
+    # overlapping x / y are refused before anything touches the device (addresses are never read)
+    base = 1 << 32
+    assert lib.rdn_forward(1, 4, ctypes.c_void_p(base), ctypes.c_void_p(base), ctypes.c_void_p(base + 4 * 999),
+                           2, 1000, None, 0, None) == -1
+    assert b"overlap" in lib.rdn_last_error()
 
 
 def _fold(sd, conv, bn):
