@@ -57,14 +57,17 @@ typedef enum {
  *              + e4m3 lo activations (~15 significant bits).  2e-2-safe at 2/3 of the MFMA cycles
  *              of RDN_BF16X3.  Activations saturate at +-1792 (the e4m3 range of hi / 4).
  *   RDN_F16    one f16 MFMA per product (v_mfma_f32_16x16x32_f16, the bf16 rate), f16 weights and
- *              activations (11 significant bits), fp32 accumulation: the fastest mode WITHIN the 2e-2
- *              bf16 bar on every golden fixture (worst 1.6e-2, trained RRCDNet).  Activations must
- *              stay below the f16 range (65504); a larger one becomes inf, never a silent wrong value.
+ *              activations (11 significant bits), fp32 accumulation: the fastest mode within the 2e-2
+ *              bf16 bar on the golden fixtures of 1DCNN, DSDN, ADSDN, PIDN and APIDN (worst 6.9e-3,
+ *              trained DSDN) -- NOT on trained RRCDNet (3.6e-2): use RDN_F16MIX there.  Activations
+ *              must stay below the f16 range (65504); a larger one becomes inf, never a silent wrong
+ *              value.
  *   RDN_F16MIX RRCDNet only: RDN_F16 arithmetic with the RDN_F16F8 correction kept on the last three
- *              layers of the right branch (the ones the head's cancellation x - (r + l)/2 amplifies),
- *              on the in-place tile: within 2e-2 (1.4e-2 on trained RRCDNet, where plain RDN_F16
- *              gives 3.5e-2).  The corrected layers are compiled in; rdn_get_correction_mask reads
- *              them back from a packed blob. */
+ *              layers of the right branch (the ones the head's cancellation x - (r + l)/2 amplifies):
+ *              within 2e-2 (1.4e-2 on trained RRCDNet).  One hybrid kernel: the plain layers on the
+ *              RDN_F16 ping-pong engine, the corrected ones and the heads on the in-place tile.  The
+ *              corrected layers are compiled in; rdn_get_correction_mask reads them back from a
+ *              packed blob. */
 typedef enum { RDN_F32 = 0, RDN_BF16 = 1, RDN_BF16X3 = 2, RDN_F16F8 = 3, RDN_F16 = 4, RDN_F16MIX = 5 } rdn_dtype;
 
 enum {
