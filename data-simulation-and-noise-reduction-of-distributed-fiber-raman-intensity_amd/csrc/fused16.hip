@@ -58,7 +58,7 @@ H16_BODY(rrcdnet) {
   float l[HN];
   head<EDGE>(tl, BUF0, F0, F1, false, l);
   // y = x - (right + left) / 2 on this tile's output rows (the lanes that stored r re-read it)
-  if ((tid() & 63) < 16) {
+  if ((tid() & 63) < HEAD_LANES) {
 #pragma unroll
     for (int k = 0; k < HN; ++k) {
       const int j = head_row(k);

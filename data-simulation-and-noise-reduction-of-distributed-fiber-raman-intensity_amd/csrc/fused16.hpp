@@ -74,34 +74,52 @@ constexpr int BIAS_OFF = H16_BIAS_OFF;
 #ifndef RDN_H16_PF
 #define RDN_H16_PF 3
 #endif
-#ifndef RDN_H16_LDSTEP
-#define RDN_H16_LDSTEP 4
-#endif
 #ifndef RDN_H16_PKRELU
 #define RDN_H16_PKRELU 1
 #endif
+// RDN_H16_M32: the layer as v_mfma_f32_32x32x16 (32 output channels x 32 positions x 16 K per
+// MFMA: half the MFMA instructions of the 16x16x32 form for the same work, so each one leaves 24 of
+// its 32 cycles of vector issue to the LDS reads, weight loads and epilogue instead of 8 of 16).
+#ifndef RDN_H16_M32
+#define RDN_H16_M32 0
+#endif
 constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
-constexpr int MH = 2;                                 // output-channel halves (2 M-tiles each)
+constexpr int MH = 2;                                 // output-channel halves (32 channels each)
 constexpr int RB = WAVES / MH;                        // row blocks
 constexpr int RW = WB / RB;                           // 160 rows per wave
-constexpr int NT = RW / 16;                           // 10 N-tiles per wave
-constexpr int HN = NT / MH;                           // head N-tiles per wave (the two halves split the rows)
-static_assert(RW % 16 == 0 && NT % MH == 0, "rows per wave must be whole N-tiles");
+#if RDN_H16_M32
+constexpr int NR = 32;                                // positions per N-tile
+constexpr int KS = 12;                                // k-steps per layer (3 taps x 4 x 16 channels)
+constexpr int NFRAG = 12;                             // A-fragments per wave per layer
+constexpr int NBIAS = 4;                              // 16-B bias loads per wave per layer
+constexpr int HEAD_LANES = 32;
+#else
+constexpr int NR = 16;
+constexpr int KS = 6;                                 // 3 taps x 2 x 32 channels
+constexpr int NFRAG = 12;                             // 2 M-tiles x 6 k-steps
+constexpr int NBIAS = 2;
+constexpr int HEAD_LANES = 16;
+#endif
+constexpr int NT = RW / NR;                           // N-tiles per wave (10 / 5)
+constexpr int HN = (NT + MH - 1) / MH;                // head N-tiles per wave (the two halves split the rows)
+static_assert(RW % NR == 0, "rows per wave must be whole N-tiles");
 static_assert((WB % 64) == 0 && (THREADS % 64) == 0, "stem items must not straddle a slot within a wave");
 
 typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 #if RDN_H16_F16
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 typedef f16x8_t V;
 typedef _Float16 E;
 __device__ __forceinline__ f32x4 mma(V a, V b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ f32x16 mma(V a, V b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
 #else
 typedef bf16x8 V;
 typedef __bf16 E;
 __device__ __forceinline__ f32x4 mma(V a, V b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ f32x16 mma(V a, V b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0); }
 #endif
-
 // Thread index the compiler cannot treat as loop-invariant (per-lane addresses are recomputed where
 // they are used instead of being hoisted across the network's layers and spilled)
 __device__ __forceinline__ int tid() {
@@ -109,7 +127,18 @@ __device__ __forceinline__ int tid() {
   asm volatile("" : "+v"(t));
   return t;
 }
+#if RDN_H16_M32
+// 32x32x16 B reads: a ds_read_b128 lane group holds 16 rows that are distinct mod 16, all at one
+// slot, so (row & 1, slot ^ f(row)) must be distinct over row mod 16 (a 128-B row spans half the
+// 64 banks); the 16-B epilogue stores (8 consecutive aligned rows per lane group, one slot) need f
+// distinct over 8 aligned rows.  f = (row & 7) ^ ((row >> 3) & 1) does both; 640 = 0 mod 16, so a
+// wrapped tap keeps the swizzle.
+__device__ __forceinline__ int soff(int row, int slot) {
+  return row * ROWB + ((slot ^ (row & 7) ^ ((row >> 3) & 1)) << 4);
+}
+#else
 __device__ __forceinline__ int soff(int row, int slot) { return row * ROWB + ((slot ^ (row & 7)) << 4); }
+#endif
 __device__ __forceinline__ int wrap(int row) { return row < 0 ? row + WB : (row >= WB ? row - WB : row); }
 __device__ __forceinline__ bool in_range(int p, int L) { return (unsigned)p < (unsigned)L; }
 // LDS-only workgroup barrier: this wave's LDS traffic drains, its global loads (next layer's
@@ -127,42 +156,100 @@ struct Tile {
   int layer;             // big layer whose fragments are in VGPRs
   // per-lane LDS offsets, computed once per tile (no address arithmetic at each layer's start):
   // koff[d + 2][u] = soff(r0 + d, 4u + q) for tap shift d in -2..2 (no wrap), r0 = this lane's
-  // first row ((w % RB) * RW + lane % 16)
-  int koff[5][2];
+  // first row ((w % RB) * RW + lane % 16); M32: koff[d + 2][v] = soff(r0 + d, 2v + lane / 32),
+  // r0 = (w % RB) * RW + lane % 32
+  int koff[5][KS / 3];
   int r0;
 };
 
-struct Frags {            // one layer's operands in VGPRs: this wave's 2 M-tiles of A-fragments and folded bias
-  V a[2][6];
-  f32x4 bias[2];
+struct Frags {            // one layer's operands in VGPRs: this wave's A-fragments and folded bias
+  V a[NFRAG];             // 16x16x32: [M-tile 2][k-step 6]; 32x32x16: [k-step 12]
+  f32x4 bias[NBIAS];
 };
-// this wave's output-channel half (M-tiles 2h, 2h + 1), wave-uniform
+// this wave's output-channel half (channels 32h .. 32h + 31), wave-uniform
 __device__ __forceinline__ int mhalf() { return __builtin_amdgcn_readfirstlane(tid() >> 6) / RB; }
 
 // Operand loads as raw buffer loads: lane offset in a VGPR, layer/fragment offset in an SGPR, so
-// the 28 loads of a layer cost no address VALU.
+// the loads of a layer cost no address VALU.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-// voff: the lane's byte offset, (lane & 63) * 16 for a fragment and (lane >> 4) * 16 for a bias,
-// computed once per layer by the caller (one opaque tid(), not one per load)
-__device__ __forceinline__ V load_frag(const Tile& tl, int layer, int m, int s, int voff) {
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, voff, layer * LAYER_BYTES + (m * 6 + s) * 1024, 0);
-  return __builtin_bit_cast(V, v);
+struct LaneOff {          // this lane's byte offsets of the A-fragment and bias loads
+  int a, b;
+};
+// One opaque tid() per layer, not one per load.  The blob's fragments are 16x16x32 A-operands,
+// fragment (m, s = 2t + u) lane r + 16q = W[16m + r][slot 4u + q of tap t] (pack.cpp).  M32 gathers
+// its 32x32x16 A-operand for k-step (t, v) from them: lane r + 32e needs cout 32h + r at slot
+// g = 2v + e, i.e. fragment (2h + r / 16, 2t + v / 2), lane (r % 16) + 16 (2 (v % 2) + e) -- a
+// per-lane part (below) plus a wave-uniform one (load_op); bias regs 4j..4j+3 of lane 32e + r are
+// couts 32h + 8j + 4e + 0..3.
+__device__ __forceinline__ LaneOff lane_off() {
+  const int lane = tid() & 63;
+#if RDN_H16_M32
+  return {((lane >> 4) & 1) * 6 * 1024 + (lane & 15) * 16 + (lane >> 5) * 256, (lane >> 5) * 16};
+#else
+  return {lane * 16, (lane >> 4) * 16};
+#endif
 }
-
-// lane quarter q's 4 output channels of M-tile m
-__device__ __forceinline__ f32x4 load_bias(const Tile& tl, int layer, int m, int voff) {
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, voff, layer * LAYER_BYTES + BIAS_OFF + 64 * m, 0);
-  return __builtin_bit_cast(f32x4, v);
+// operand i of half h of big layer `layer`: A-fragment i (< NFRAG) or bias vector i - NFRAG
+__device__ __forceinline__ void load_op(const Tile& tl, int layer, int h, int i, const LaneOff& lo, Frags& F) {
+  const int base = layer * LAYER_BYTES;
+  if (i < NFRAG) {
+#if RDN_H16_M32
+    const int t = i >> 2, v = i & 3;
+    const int so = base + (12 * h + 2 * t + (v >> 1)) * 1024 + (v & 1) * 512;
+#else
+    const int so = base + ((2 * h + i / 6) * 6 + i % 6) * 1024;
+#endif
+    F.a[i] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, lo.a, so, 0));
+  } else {
+    const int j = i - NFRAG;
+#if RDN_H16_M32
+    const int so = base + BIAS_OFF + 128 * h + 32 * j;
+#else
+    const int so = base + BIAS_OFF + 64 * (2 * h + j);
+#endif
+    F.bias[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, lo.b, so, 0));
+  }
 }
+constexpr int NLOAD = NFRAG + NBIAS;
 
 __device__ __forceinline__ void load_frags(const Tile& tl, int layer, Frags& F) {
-  const int lane = tid() & 63, fv = lane * 16, bv = (lane >> 4) * 16, mt = 2 * mhalf();
+  const LaneOff lo = lane_off();
+  const int h = mhalf();
+#pragma unroll
+  for (int i = 0; i < NLOAD; ++i) load_op(tl, layer, h, i, lo, F);
+}
+
+// Accumulators of one N-tile: 16x16x32: M-tiles 2h, 2h + 1 (16 channels x 16 positions each);
+// 32x32x16: one 32 x 32 tile.  Start at the folded bias.
+struct Acc {
+#if RDN_H16_M32
+  f32x16 v;
+#else
+  f32x4 v[2];
+#endif
+};
+__device__ __forceinline__ void mstep(const Frags& F, int s, V b, Acc& acc) {
+#if RDN_H16_M32
+  const f32x16 bias = __builtin_shufflevector(__builtin_shufflevector(F.bias[0], F.bias[1], 0, 1, 2, 3, 4, 5, 6, 7),
+                                              __builtin_shufflevector(F.bias[2], F.bias[3], 0, 1, 2, 3, 4, 5, 6, 7),
+                                              0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+#if defined(RDN_ABLATE_NOMFMA)
+  if (s == 0) acc.v = bias;
+  asm volatile("" : "+v"(acc.v) : "v"(F.a[s]), "v"(b));
+#else
+  acc.v = mma(F.a[s], b, s == 0 ? bias : acc.v);
+#endif
+#else
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
-    F.bias[m] = load_bias(tl, layer, mt + m, bv);
-#pragma unroll
-    for (int s = 0; s < 6; ++s) F.a[m][s] = load_frag(tl, layer, mt + m, s, fv);
+#if defined(RDN_ABLATE_NOMFMA)
+    if (s == 0) acc.v[m] = F.bias[m];
+    asm volatile("" : "+v"(acc.v[m]) : "v"(F.a[m * 6 + s]), "v"(b));
+#else
+    acc.v[m] = mma(F.a[m * 6 + s], b, s == 0 ? F.bias[m] : acc.v[m]);
+#endif
   }
+#endif
 }
 
 // Conv1d(1, 64, 3, padding=1) (+ folded BN) + ReLU in fp32: one (row, 16-B slot) item per lane,
@@ -205,46 +292,51 @@ enum Epi : int {
   RES_RELU = 2,   // relu(acc + b + dst)    (DSDN ResidualBlock: out += identity; relu)
 };
 
-// LDS byte addresses of this lane's B fragment for k-step s = (tap t, half u) of N-tile n, from
-// the tile's per-lane offsets: a tap shift keeps the (row & 7) swizzle of a 640-row wrap (640 = 0
-// mod 8), so the wrapped taps of the first / last wave (only (n = 0, t = 0) and (n = NT-1, t = 2)
-// can leave the tile) are the unwrapped offset -/+ one buffer.
+// LDS byte addresses of this lane's B fragment for k-step s = (tap t, part u) of N-tile n, from
+// the tile's per-lane offsets: a tap shift keeps the swizzle of a 640-row wrap (640 = 0 mod 16),
+// so the wrapped taps of the first / last wave (only (n = 0, t = 0) and (n = NT-1, t = 2) can leave
+// the tile) are the unwrapped offset -/+ one buffer.
 struct BAddr {
-  int m[6], first[2], last[2];
+  static constexpr int U = KS / 3;      // k-steps per tap
+  int m[KS], first[U], last[U];
   __device__ __forceinline__ BAddr(const Tile& tl, uint32_t src, int dil) {
     const bool d1 = dil == 1;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) {
       m[u] = (int)src + (d1 ? tl.koff[1][u] : tl.koff[0][u]);
-      m[2 + u] = (int)src + tl.koff[2][u];
-      m[4 + u] = (int)src + (d1 ? tl.koff[3][u] : tl.koff[4][u]);
+      m[U + u] = (int)src + tl.koff[2][u];
+      m[2 * U + u] = (int)src + (d1 ? tl.koff[3][u] : tl.koff[4][u]);
     }
-    const bool wl = tl.r0 < dil, wh = tl.r0 + 16 * (NT - 1) + dil >= WB;
+    const bool wl = tl.r0 < dil, wh = tl.r0 + NR * (NT - 1) + dil >= WB;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) {
       first[u] = m[u] + (wl ? (int)BUF_BYTES : 0);
-      last[u] = m[4 + u] + 16 * (NT - 1) * ROWB - (wh ? (int)BUF_BYTES : 0);
+      last[u] = m[2 * U + u] + NR * (NT - 1) * ROWB - (wh ? (int)BUF_BYTES : 0);
     }
   }
   __device__ __forceinline__ int at(int n, int s) const {
-    const int t = s >> 1, u = s & 1;
+    const int t = s / U, u = s % U;
     if (n == 0 && t == 0) return first[u];
     if (n == NT - 1 && t == 2) return last[u];
-    return m[s] + n * 16 * ROWB;
+    return m[s] + n * NR * ROWB;
   }
 };
 
-// One Conv1d(64, 64, 3, dilation=dil, padding=dil) over the tile, src -> dst: this wave's 2 M-tiles
-// x 10 N-tiles from the operands in F, while the next layer's operands stream into G (header).
+#ifndef RDN_H16_LDSTEP
+#define RDN_H16_LDSTEP (RDN_H16_M32 ? 3 : 4)
+#endif
+static_assert(RDN_H16_LDSTEP * (NLOAD - 1) < KS * NT, "every operand load of the next layer must be issued");
+
+// One Conv1d(64, 64, 3, dilation=dil, padding=dil) over the tile, src -> dst: this wave's 32
+// output channels x NT N-tiles from the operands in F, while the next layer's operands stream into
+// G (header).
 template <int EPI, bool EDGE>
 __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int dil, const Frags& F, Frags& G,
                                       bool has_next = true) {
-  const int lane = tid() & 63, w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB, q = lane >> 4,
-            c16 = lane & 15;
-  const int next = tl.layer + 1, mt = 2 * h;
+  const int lane = tid() & 63, w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB;
+  const int next = tl.layer + 1;
   asm volatile("" : "+s"(src), "+s"(dst));   // per-layer addresses: not hoisted out of a network's loop (spills)
   const BAddr ba(tl, src, dil);
-  const int sa = (int)dst + (h ? tl.koff[2][1] : tl.koff[2][0]);     // slot 4h + q of row r0
   const int pos0 = tl.base + (w % RB) * RW;
 
   // Idle waves of a short last tile: every row of this wave lies at position >= L + 2, beyond the
@@ -258,13 +350,10 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     lds_barrier();
     return;
   }
+  const LaneOff lo = lane_off();
 
-  // bias (+ identity), ReLU, zero rows outside [0, L), round, store the 8 channels of M-tiles
-  // 2h, 2h+1 of N-tile n as one 16-B slot
-  auto epilogue = [&](int n, const f32x4& a0, const f32x4& a1) {
-    const bool valid = !EDGE || in_range(pos0 + 16 * n + c16, tl.L);
-    f32x8 v = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
-    V* p = (V*)(tl.lds + sa + n * 16 * ROWB);
+  // bias (+ identity), ReLU, zero rows outside [0, L), round, store 8 channels as one 16-B slot
+  auto store_slot = [&](V* p, f32x8 v, bool valid) {
     if (EPI == RES_RELU) v += __builtin_convertvector(*p, f32x8);
 #if RDN_H16_F16 && RDN_H16_PKRELU
     // ReLU after the rounding, on packed f16 (4 v_pk_max_f16 instead of 8 v_max_f32; the rounding is
@@ -285,57 +374,54 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     *p = __builtin_convertvector(v, V);
 #endif
   };
+#if RDN_H16_M32
+  // lane r + 32e holds channels 32h + (i & 3) + 8 (i >> 2) + 4e of position r in acc reg i: regs
+  // 0-3, 8-11 are slot 4h + e, regs 4-7, 12-15 slot 4h + 2 + e (h16_channel order)
+  const int sa0 = (int)dst + (h ? tl.koff[2][2] : tl.koff[2][0]), sa1 = (int)dst + (h ? tl.koff[2][3] : tl.koff[2][1]);
+  auto epilogue = [&](int n, const Acc& a) {
+    const bool valid = !EDGE || in_range(pos0 + NR * n + (lane & 31), tl.L);
+    store_slot((V*)(tl.lds + sa0 + n * NR * ROWB), __builtin_shufflevector(a.v, a.v, 0, 1, 2, 3, 8, 9, 10, 11), valid);
+    store_slot((V*)(tl.lds + sa1 + n * NR * ROWB), __builtin_shufflevector(a.v, a.v, 4, 5, 6, 7, 12, 13, 14, 15), valid);
+  };
+#else
+  const int sa = (int)dst + (h ? tl.koff[2][1] : tl.koff[2][0]);     // slot 4h + q of row r0
+  auto epilogue = [&](int n, const Acc& a) {
+    const bool valid = !EDGE || in_range(pos0 + NR * n + (lane & 15), tl.L);
+    store_slot((V*)(tl.lds + sa + n * NR * ROWB), __builtin_shufflevector(a.v[0], a.v[1], 0, 1, 2, 3, 4, 5, 6, 7), valid);
+  };
+#endif
 
-  f32x4 prev[2];
+  Acc prev;
   constexpr int PF = RDN_H16_PF;       // B fragments in flight ahead of the step that consumes them
-  constexpr int K = 6 * NT;            // steps (N-tile n, k-step s), k = 6n + s
+  constexpr int K = KS * NT;           // steps (N-tile n, k-step s), k = KS n + s
   V B[PF + 1];
 #pragma unroll
-  for (int k = 0; k < PF; ++k) B[k] = *(const V*)(tl.lds + ba.at(k / 6, k % 6));
+  for (int k = 0; k < PF; ++k) B[k] = *(const V*)(tl.lds + ba.at(k / KS, k % KS));
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
-    f32x4 acc[2];
+    Acc acc;
 #pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int k = 6 * n + s, kp = k + PF;
+    for (int s = 0; s < KS; ++s) {
+      const int k = KS * n + s, kp = k + PF;
 #if defined(RDN_ABLATE_NOLDS)
       if (kp < K) { B[kp % (PF + 1)] = B[(k + 1) % (PF + 1)]; asm volatile("" : "+v"(B[kp % (PF + 1)])); }
 #else
-      if (kp < K) B[kp % (PF + 1)] = *(const V*)(tl.lds + ba.at(kp / 6, kp % 6));
+      if (kp < K) B[kp % (PF + 1)] = *(const V*)(tl.lds + ba.at(kp / KS, kp % KS));
 #endif
-      const V b = B[k % (PF + 1)];
-#pragma unroll
-      for (int m = 0; m < 2; ++m) {
-#if defined(RDN_ABLATE_NOMFMA)
-        if (s == 0) acc[m] = F.bias[m];
-        asm volatile("" : "+v"(acc[m]) : "v"(F.a[m][s]), "v"(b));
-#else
-        acc[m] = mma(F.a[m][s], b, s == 0 ? F.bias[m] : acc[m]);
-#endif
-      }
-      if (n > 0 && s == 1) epilogue(n - 1, prev[0], prev[1]);
+      mstep(F, s, B[k % (PF + 1)], acc);
+      if (n > 0 && s == 1) epilogue(n - 1, prev);
 #if !defined(RDN_ABLATE_NOALOAD)
-      // the next layer's 12 fragments + 2 bias vectors, one buffer load every LDSTEP-th step: the
-      // vector-memory traffic of the CU's 8 waves spreads over the layer (denser is slower: 2 steps
-      // -2 %, 3 steps -0.5 % against 4)
+      // the next layer's operands, one buffer load every LDSTEP-th step: the vector-memory traffic
+      // of the CU's 8 waves spreads over the layer (16x16x32: denser is slower, 2 steps -2 %,
+      // 3 steps -0.5 % against 4)
       constexpr int LDSTEP = RDN_H16_LDSTEP;
-      if (has_next && k % LDSTEP == 0 && k / LDSTEP < 14) {
-        const int i = k / LDSTEP;
-#if defined(RDN_ABLATE_ALOAD_LDS)          // diagnostic: the same VGPR traffic from LDS instead of L1/L2
-        if (i < 12) G.a[i / 6][i % 6] = *(const V*)(tl.lds + 16 * lane + 1024 * i);
-        else G.bias[i - 12] = *(const f32x4*)(tl.lds + 16 * lane + 1024 * i);
-#else
-        if (i < 12) G.a[i / 6][i % 6] = load_frag(tl, next, mt + i / 6, i % 6, 16 * lane);
-        else G.bias[i - 12] = load_bias(tl, next, mt + i - 12, 16 * q);
-#endif
-      }
+      if (has_next && k % LDSTEP == 0 && k / LDSTEP < NLOAD) load_op(tl, next, h, k / LDSTEP, lo, G);
 #endif
       __builtin_amdgcn_sched_barrier(0);
     }
-    prev[0] = acc[0];
-    prev[1] = acc[1];
+    prev = acc;
   }
-  epilogue(NT - 1, prev[0], prev[1]);
+  epilogue(NT - 1, prev);
   tl.layer += 1;
 #if defined(RDN_ABLATE_NOBARRIER)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -344,19 +430,20 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
 #endif
 }
 
-// Conv1d(64, 1, 3) head, packed as a big layer whose M-tiles 0 and 2 both hold cout 0 in row 0 and
-// its weights' rounding residue in row 1 (pack.cpp pack_big_bf16: the two partial sums add in fp32,
-// so the head's weights are exact to ~2^-22 at no extra MFMA; the head feeds the RRCDNet
-// cancellation x - (r + l)/2).  Half h computes N-tiles h*HN .. h*HN + HN-1 of its row block from
-// M-tile 2h (F.a[0]); out[j] = cout 0 of row head_row(j), in lanes 0..15.  No write, no barrier;
-// the next layer's operands stream into G.
+// Conv1d(64, 1, 3) head, packed as a big layer whose M-tiles 0 and 2 (channels 0 and 32) both hold
+// cout 0 in row 0 and its weights' rounding residue in row 1 (pack.cpp pack_big_bf16: the two
+// partial sums add in fp32, so the head's weights are exact to ~2^-22 at no extra MFMA; the head
+// feeds the RRCDNet cancellation x - (r + l)/2).  Half h computes N-tiles h*HN .. h*HN + HN-1 of
+// its row block (those < NT) from its first M-tile / its 32-channel tile; out[j] = cout 0 of row
+// head_row(j), in lanes 0..HEAD_LANES-1 (regs 0 and 1 hold rows 0 and 1 there in both MFMA forms).
+// No write, no barrier; the next layer's operands stream into G.
 template <bool EDGE>
 __device__ __forceinline__ void head(Tile& tl, uint32_t src, const Frags& F, Frags& G, bool has_next,
                                      float (&out)[HN]) {
-  const int lane = tid() & 63, w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB, q = lane >> 4;
-  const int next = tl.layer + 1, mt = 2 * h;
+  const int w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB;
+  const int next = tl.layer + 1;
   const BAddr ba(tl, src, 1);
-  const int pos0 = tl.base + (w % RB) * RW + 16 * HN * h;
+  const int pos0 = tl.base + (w % RB) * RW + NR * HN * h;
   if (EDGE && pos0 >= tl.L + 2) {
     if (has_next) load_frags(tl, next, G);
 #pragma unroll
@@ -364,34 +451,36 @@ __device__ __forceinline__ void head(Tile& tl, uint32_t src, const Frags& F, Fra
     tl.layer += 1;
     return;
   }
-  // N-tile h*HN + j: only (j = 0, t = 0) of half 0 and (j = HN-1, t = 2) of half 1 can leave the tile
-  auto addr = [&](int j, int s) {
-    const int t = s >> 1, u = s & 1;
-    const int plain = ba.m[s] + (h * HN + j) * 16 * ROWB;
-    if (j == 0 && t == 0) return h == 0 ? ba.first[u] : plain;
-    if (j == HN - 1 && t == 2) return h == MH - 1 ? ba.last[u] : plain;
-    return plain;
-  };
-  constexpr int PF = RDN_H16_PF, K = 6 * HN;
+  const LaneOff lo = lane_off();
+  // N-tile of step j, clamped (the reads of a skipped N-tile stay inside the buffer)
+  auto ntile = [&](int j) { return min(h * HN + j, NT - 1); };
+  constexpr int PF = RDN_H16_PF, K = KS * HN;
   V B[PF + 1];
 #pragma unroll
-  for (int k = 0; k < PF; ++k) B[k] = *(const V*)(tl.lds + addr(k / 6, k % 6));
+  for (int k = 0; k < PF; ++k) B[k] = *(const V*)(tl.lds + ba.at(ntile(k / KS), k % KS));
 #pragma unroll
   for (int j = 0; j < HN; ++j) {
-    f32x4 acc;
+    Acc acc;
+    const bool live = h * HN + j < NT;     // wave-uniform
 #pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int k = 6 * j + s, kp = k + PF;
-      if (kp < K) B[kp % (PF + 1)] = *(const V*)(tl.lds + addr(kp / 6, kp % 6));
-      acc = mma(F.a[0][s], B[k % (PF + 1)], s == 0 ? F.bias[0] : acc);
-      if (has_next && k % 2 == 0 && k / 2 < 14) {
-        const int i = k / 2;
-        if (i < 12) G.a[i / 6][i % 6] = load_frag(tl, next, mt + i / 6, i % 6, 16 * lane);
-        else G.bias[i - 12] = load_bias(tl, next, mt + i - 12, 16 * q);
+    for (int s = 0; s < KS; ++s) {
+      const int k = KS * j + s, kp = k + PF;
+      if (kp < K) B[kp % (PF + 1)] = *(const V*)(tl.lds + ba.at(ntile(kp / KS), kp % KS));
+      if (live) {
+#if RDN_H16_M32
+        acc.v = mma(F.a[s], B[k % (PF + 1)], s == 0 ? __builtin_shufflevector(F.bias[0], F.bias[0], 0, 1, 2, 3, 0, 1, 2, 3, 0, 1, 2, 3, 0, 1, 2, 3) : acc.v);
+#else
+        acc.v[0] = mma(F.a[s], B[k % (PF + 1)], s == 0 ? F.bias[0] : acc.v[0]);
+#endif
       }
+      if (has_next && k % 2 == 0 && k / 2 < NLOAD) load_op(tl, next, h, k / 2, lo, G);
       __builtin_amdgcn_sched_barrier(0);
     }
-    out[j] = acc[0] + acc[1];
+#if RDN_H16_M32
+    out[j] = live ? acc.v[0] + acc.v[1] : 0.f;
+#else
+    out[j] = acc.v[0][0] + acc.v[0][1];
+#endif
   }
   tl.layer += 1;
 }
@@ -411,23 +500,34 @@ __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const 
   // 32-bit data format of the gfx9 buffer descriptor)
   tl.wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)tl.big, 0, 0x7fffffff, 0x00020000);
   tl.layer = 0;
-  const int t = tid(), q = (t & 63) >> 4;
+  const int t = tid();
+#if RDN_H16_M32
+  const int e = (t & 63) >> 5;
+  tl.r0 = ((t >> 6) % RB) * RW + (t & 31);
+#pragma unroll
+  for (int d = -2; d <= 2; ++d)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) tl.koff[d + 2][v] = soff(tl.r0 + d, 2 * v + e);
+#else
+  const int q = (t & 63) >> 4;
   tl.r0 = ((t >> 6) % RB) * RW + (t & 15);
 #pragma unroll
   for (int d = -2; d <= 2; ++d)
 #pragma unroll
     for (int u = 0; u < 2; ++u) tl.koff[d + 2][u] = soff(tl.r0 + d, 4 * u + q);
+#endif
   return tl;
 }
 
-// tile row of head output j of this lane (lanes 0..15)
+// tile row of head output j of this lane (lanes 0..HEAD_LANES-1); a row no tile owns (WB) for the
+// skipped N-tile of an odd NT
 __device__ __forceinline__ int head_row(int j) {
-  const int w = tid() >> 6;
-  return (w % RB) * RW + 16 * (HN * (w / RB) + j) + (tid() & 15);
+  const int w = tid() >> 6, n = HN * (w / RB) + j;
+  return n < NT ? (w % RB) * RW + NR * n + (tid() & (HEAD_LANES - 1)) : WB;
 }
 
 __device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, const float (&v)[HN], int halo, int T) {
-  if ((tid() & 63) >= 16) return;
+  if ((tid() & 63) >= HEAD_LANES) return;
 #pragma unroll
   for (int k = 0; k < HN; ++k) {
     const int j = head_row(k);

@@ -147,6 +147,9 @@ int big_layers(const std::vector<Op>& spec, int dtype) {
   const bool head_big = lay == BF16 || lay == F16;
   int n = 0;
   for (const Op& o : spec) n += o.kind == OpKind::BIG || (o.kind == OpKind::HEAD && head_big);
+  // RDN_F16MIX: the last head (RRCDNet's left_net.19) also as a ping-pong head record after the big
+  // layers (fused_inplace.hip rrcdnet_hybrid runs the left branch on the ping-pong engine)
+  if (dtype == F16MIX) ++n;
   return n;
 }
 
@@ -377,6 +380,16 @@ static void pack_big_h8(const Folded& f, uint8_t* dst) {
   for (int c = 0; c < C; ++c) bias[c] = c < f.cout ? (float)f.b[c] : 0.f;
 }
 
+// a head as fused16's head record (f16 fragments with the rounding residue in row 1, pack_big_bf16)
+// inside an f16 + e4m3-sized record: the ping-pong engine reads the H8 blob with that record stride
+// and its bias at H8_BIAS_OFF
+static void pack_head_h8(const Folded& f, uint8_t* dst) {
+  std::vector<uint8_t> rec(BIG_BYTES_BF16);
+  pack_big_bf16(f, rec.data(), true);
+  std::memcpy(dst, rec.data(), BIG_FRAG_BYTES_BF16);
+  std::memcpy(dst + H8_BIAS_OFF, rec.data() + BIG_FRAG_BYTES_BF16, C * sizeof(float));
+}
+
 static void pack_small_conv(const Folded& f, float* slot) {   // w[c*3+t], bias at 192 (+c)
   std::memset(slot, 0, SMALL_SLOT_FLOATS * sizeof(float));
   if (f.cin == 1) {
@@ -468,6 +481,7 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
         if (!fold(rd, o, C, 1, f)) return rd.err;
         pack_small_conv(f, small + o.slot * SMALL_SLOT_FLOATS);
         if (layout == BF16 || layout == F16) pack_big_bf16(f, big + (layer++) * big_bytes, layout == F16);
+        else if (dtype == F16MIX && &o == &spec.back()) pack_head_h8(f, big + (layer++) * big_bytes);
         break;
       case OpKind::CBAM:
         if (!pack_cbam(rd, o, small)) return rd.err;

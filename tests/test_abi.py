@@ -223,12 +223,45 @@ def test_pack_layout_f16f8():
     assert err.max() <= 2.0 ** -14 * np.abs(w64).max(), err.max()
 
 
+def test_pack_layout_f16mix_head_record():
+    """RDN_F16MIX blob: the 29 f16 + e4m3 big layers, then the left head (left_net.19) as a ping-pong head
+    record in an f16 + e4m3-sized slot: f16 fragments with cout 0 in rows 0 and 32 (M-tiles 0 and 2)
+    and its weights' f16 rounding residue in rows 1 and 33, the bias at H8_BIAS_OFF (fused16.hpp head,
+    read by fused_inplace.hip rrcdnet_hybrid)."""
+    from raman_mi355x import engine
+    sd = golden_state_dict("RRCDNet", "trained")
+    blob = engine.pack("RRCDNet", sd, "f16mix", "cpu").numpy()
+    assert blob.size == engine.packed_size("RRCDNet", "f16mix") == SMALL + 30 * 50432
+    # the big layers are the f16f8 blob's
+    ref = engine.pack("RRCDNet", sd, "f16f8", "cpu").numpy()
+    np.testing.assert_array_equal(blob[SMALL:SMALL + 29 * 50432], ref[SMALL:])
+    w, b = _fold(sd, "left_net.19", None)            # [1, 64, 3]
+    R = blob[SMALL + 29 * 50432:]
+    frag = R[:24576].view(np.float16).reshape(4, 6, 64, 8)
+    lane = np.arange(64)
+    for s_ in range(6):
+        t, u = s_ >> 1, s_ & 1
+        for j in range(8):
+            cin = 32 * u + 4 * (lane >> 4) + (j & 3) + 16 * (j >> 2)
+            exp = w[0, cin, t]
+            for m in (0, 2):
+                rows = lane & 15
+                got = frag[m, s_, :, j]
+                np.testing.assert_array_equal(got[rows == 0], exp[rows == 0].astype(np.float16))
+                res = (exp.astype(np.float64) - exp.astype(np.float16).astype(np.float64))
+                np.testing.assert_array_equal(got[rows == 1], res[rows == 1].astype(np.float16))
+                assert np.all(got[rows >= 2] == 0)
+            assert np.all(frag[1, s_] == 0) and np.all(frag[3, s_] == 0)
+    bias = R[50176:].view(np.float32)
+    assert bias[0] == b[0] and bias[32] == b[0] and np.count_nonzero(bias) <= 2
+
+
 def _fold_f64(sd, conv):
     return sd[conv + ".weight"].double().numpy()
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("arch,dtype", [("RRCDNet", "f16f8"), ("ADSDN", "fp32"), ("DSDN", "bf16x3"),
+@pytest.mark.parametrize("arch,dtype", [("RRCDNet", "f16f8"), ("RRCDNet", "f16mix"), ("ADSDN", "fp32"), ("DSDN", "bf16x3"),
                                         ("APIDN", "bf16-unsafe"), ("DenoiseCNN", "f16f8")])
 def test_host_sanitizer_pack(arch, dtype, tmp_path):
     """pack.cpp + abi.cpp built with ASan + UBSan (csrc/Makefile `asan`): packing a

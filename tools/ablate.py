@@ -25,7 +25,8 @@ VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "hibase0": "-DRDN_IP_HIBASE=0", "dsdn3": "-DRDN_DSDN_NBK=3", "comp0": "-DRDN_F32_COMP=0",
             "chunk1": "-DRDN_F32_CHUNK=1", "chunk3": "-DRDN_F32_CHUNK=3", "chunk4": "-DRDN_F32_CHUNK=4",
             "h16f16": "-DRDN_H16_F16=1", "h8plain": "-DRDN_ABLATE_H8_PLAIN", "nohead": "-DRDN_ABLATE_NOHEAD",
-            "mixold": "-DRDN_F16MIX_HYBRID=0", "pkrelu0": "-DRDN_H16_PKRELU=0", "ld2": "-DRDN_H16_LDSTEP=2", "ld4": "-DRDN_H16_LDSTEP=4", "alds": "-DRDN_ABLATE_ALOAD_LDS"}
+            "mixold": "-DRDN_F16MIX_HYBRID=0", "pkrelu0": "-DRDN_H16_PKRELU=0", "ld2": "-DRDN_H16_LDSTEP=2", "ld4": "-DRDN_H16_LDSTEP=4", "m32": "-DRDN_H16_M32=1",
+            "m32ld2": "-DRDN_H16_M32=1 -DRDN_H16_LDSTEP=2", "m32pf2": "-DRDN_H16_M32=1 -DRDN_H16_PF=2"}
 
 
 def build():

@@ -62,8 +62,9 @@ def rrcdnet(sd, x, corrected, head, term="both"):
     def store(y, k):
         """activation as the consumer of layer k's output sees it"""
         last = k in (14, 28)
-        if last:
-            return {"f16": f16, "split": e4m3_split, "fused": f32}[head](y)
+        if last:     # head: one mode for both heads, or "right/left"
+            hm = head.split("/")
+            return {"f16": f16, "split": e4m3_split, "fused": f32}[hm[0] if k == 14 or len(hm) == 1 else hm[1]](y)
         return f32(y) if (k + 1) in corrected and term != "w" else f16(y)
 
     def branch(stem_conv, stem_bn, ks, head_conv):
@@ -113,11 +114,14 @@ def main():
                ({14}, "fused", "both"), ({13, 14, 28}, "fused", "both"),
                ({12, 13, 14}, "split", "x"), ({12, 13, 14}, "split", "w"), ({11, 12, 13, 14}, "split", "x"),
                ({10, 11, 12, 13, 14}, "split", "x")]
-    if len(sys.argv) > 1:
+    if len(sys.argv) > 1 and sys.argv[1] == "heads":
+        configs = [({12, 13, 14}, "split/f16", "both"), ({12, 13, 14}, "f16/split", "both"), ({12, 13, 14}, "f16", "both"),
+                   ({11, 12, 13, 14}, "f16", "both"), ({12, 13, 14, 28}, "split/f16", "both")]
+    elif len(sys.argv) > 1:
         configs = [c for c in configs if c[2] != "both"]
     for corrected, head, term in configs:
         w = worst(corrected, head, data, term)
-        print(f"corrected {sorted(corrected)!s:20s} ({term:4s}) head {head:5s}: " +
+        print(f"corrected {sorted(corrected)!s:20s} ({term:4s}) head {head:9s}: " +
               "  ".join(f"{k} {v:.3e}" for k, v in w.items()), flush=True)
 
 
