@@ -189,9 +189,26 @@ __device__ __forceinline__ LaneOff lane_off() {
   return {lane * 16, (lane >> 4) * 16};
 #endif
 }
+// RDN_H16_LDORDER 1: the next layer's operands are fetched in the order its first N-tile consumes
+// them (the bias vectors, the C operand of its first MFMAs, first; then the fragments k-step by
+// k-step), so the waits at a layer's start cover only the oldest loads
+#ifndef RDN_H16_LDORDER
+#define RDN_H16_LDORDER 0
+#endif
 // operand i of half h of big layer `layer`: A-fragment i (< NFRAG) or bias vector i - NFRAG
 __device__ __forceinline__ void load_op(const Tile& tl, int layer, int h, int i, const LaneOff& lo, Frags& F) {
+#if RDN_H16_LDORDER && !RDN_H16_M32
+  i = i < NBIAS ? NFRAG + i : (i - NBIAS) % 2 * 6 + (i - NBIAS) / 2;
+#elif RDN_H16_LDORDER
+  i = i < NBIAS ? NFRAG + i : i - NBIAS;
+#endif
   const int base = layer * LAYER_BYTES;
+#if defined(RDN_ABLATE_WSAME)             // diagnostic (wrong results): both halves fetch half 0's operands
+  h = 0;
+#endif
+#if defined(RDN_ABLATE_WHALF)             // diagnostic (wrong results): half the fragment loads
+  if (i < NFRAG && (i & 1)) return;
+#endif
   if (i < NFRAG) {
 #if RDN_H16_M32
     const int t = i >> 2, v = i & 3;

@@ -26,7 +26,9 @@ VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "chunk1": "-DRDN_F32_CHUNK=1", "chunk3": "-DRDN_F32_CHUNK=3", "chunk4": "-DRDN_F32_CHUNK=4",
             "h16f16": "-DRDN_H16_F16=1", "h8plain": "-DRDN_ABLATE_H8_PLAIN", "nohead": "-DRDN_ABLATE_NOHEAD",
             "mixold": "-DRDN_F16MIX_HYBRID=0", "pkrelu0": "-DRDN_H16_PKRELU=0", "ld2": "-DRDN_H16_LDSTEP=2", "ld4": "-DRDN_H16_LDSTEP=4", "m32": "-DRDN_H16_M32=1",
-            "m32ld2": "-DRDN_H16_M32=1 -DRDN_H16_LDSTEP=2", "m32pf2": "-DRDN_H16_M32=1 -DRDN_H16_PF=2"}
+            "m32ld2": "-DRDN_H16_M32=1 -DRDN_H16_LDSTEP=2", "m32pf2": "-DRDN_H16_M32=1 -DRDN_H16_PF=2",
+            "ord": "-DRDN_H16_LDORDER=1", "ordld3": "-DRDN_H16_LDORDER=1 -DRDN_H16_LDSTEP=3", "ordld2": "-DRDN_H16_LDORDER=1 -DRDN_H16_LDSTEP=2",
+            "wsame": "-DRDN_ABLATE_WSAME", "whalf": "-DRDN_ABLATE_WHALF"}
 
 
 def build():
