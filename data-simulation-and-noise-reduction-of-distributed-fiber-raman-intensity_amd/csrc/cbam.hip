@@ -20,6 +20,13 @@
 
 #include "inplace.hpp"
 #include "host_util.hpp"
+// the ping-pong engine (fused16.hpp) in f16 over the blob's ping-pong section (pack.cpp
+// has_pp16_section): the convs of the RDN_F16 team kernel (team16_forward below)
+#define RDN_H16_F16 1
+#define H16_NS h16c
+#define H16_LAYER_BYTES BIG_BYTES_BF16
+#define H16_BIAS_OFF BIG_FRAG_BYTES_BF16
+#include "fused16.hpp"
 
 namespace rdn {
 namespace cb {
@@ -299,6 +306,9 @@ constexpr int STAT_BYTES = 64 * 8 + 64 * 4;        // per-tile stats: 64 fp64 su
 constexpr int SLOT_BYTES = STAT_BYTES + 2 * EDGE_BYTES;   // + the tile's first / last EDGE_ROWS own-edge rows
 static_assert(2 * TEAM_HALO - EDGE_ROWS >= TEAM_HALO - 1 && TEAM_HALO >= 4, "edge rows lie in the tile's own rows");
 constexpr unsigned SPIN_LIMIT = 1u << 22;          // ~0.3 s of s_sleep polls
+#ifndef RDN_TEAM_SLEEP
+#define RDN_TEAM_SLEEP 8                           // s_sleep units (64 clocks) between two polls
+#endif
 constexpr int TEAM_CTR_STRIDE = 16;                // u32s between team counters (64 B)
 
 struct TeamArgs {
@@ -526,7 +536,7 @@ __device__ __forceinline__ void team_wait(const TeamArgs& ta, unsigned* ctr, uns
   if (__builtin_amdgcn_workitem_id_x() == 0) {
     unsigned it = 0;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(8);
+      __builtin_amdgcn_s_sleep(RDN_TEAM_SLEEP);
       if ((++it & 63) == 0 && __hip_atomic_load(ta.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
       if (it > SPIN_LIMIT) {
         __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -823,6 +833,389 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
     for (int k = 0; k < NSTAMP; ++k) ta.stamps[(size_t)__builtin_amdgcn_workgroup_id_x() * NSTAMP + k] = stamp.acc[k];
 }
 
+
+// ---- team-persistent forward on the ping-pong engine (RDN_F16) ------------------------------------
+//
+// The same team protocol as team_forward (statistics + edge rows published per tile, one counter
+// barrier per CBAM, deterministic slot reduction, spin limit -> error word), with the convs on the
+// f16 ping-pong engine of fused16.hpp: 640-row tiles (T = 628 own positions, TEAM_HALO = 6 per
+// side: 16 tiles per spectrum at L = 10,000), two 80 KiB activation buffers, one barrier per conv.
+// Every CBAM's input u ends in BUF0; BUF1 is free during the CBAM and holds its scratch.  The
+// ResidualBlock identity (the block input, which conv2 overwrites in BUF0) is saved by conv2's
+// epilogue (fused16.hpp LINEAR_SAVE) into 10 x 8 f16 per lane, in that epilogue's (row, slot)
+// layout, which every pointwise pass of the CBAM below uses: lane (w, q, c16) owns rows
+// 160 (w % 4) + 16 n + c16 (n < 10) at 16-B slot 4 (w / 4) + q, i.e. channels h16_channel(slot, j).
+// Statistics in fp32 per lane, fp64 across waves and tiles; ca / sa in fp32; u, h and the identity
+// are f16 (the mode's storage).  ADSDN/train.py:72-167, APIDN/train.py:72-159.
+namespace t16 {
+using V = h16c::V;
+constexpr int WB16 = h16c::WB;
+constexpr int NT = h16c::NT;
+constexpr int EDGE16_BYTES = EDGE_ROWS * h16c::ROWB;        // one edge, f16 rows
+constexpr int SLOT16_BYTES = STAT_BYTES + 2 * EDGE16_BYTES;
+// CBAM scratch in BUF1
+constexpr int SC = h16c::BUF1;
+constexpr int RED16_OFF = SC;                                  // [4 row blocks][64] f32 sums, then u32 maxima
+constexpr int SLP_OFF = RED16_OFF + 2 * 4 * 64 * 4;            // [8 waves][64] f64 slot partials, then u32
+constexpr int POOL_OFF = SLP_OFF + 8 * 64 * 12;                // [2][64] f64: pooled avg / max
+constexpr int H1_16_OFF = POOL_OFF + 2 * 64 * 8;               // MLP hidden (8 f32)
+constexpr int CA16_OFF = H1_16_OFF + 64;                       // channel attention (64 f32)
+constexpr int S1H_OFF = CA16_OFF + 64 * 4;                     // [2 halves][WB16] partial sums over 32 channels
+constexpr int S2H_OFF = S1H_OFF + 2 * WB16 * 4;                // [2 halves][WB16] partial maxima
+constexpr int SA16_OFF = S2H_OFF + 2 * WB16 * 4;               // spatial attention per tile row
+constexpr int M1_OFF = SA16_OFF + WB16 * 4;                    // [mean_c; max_c] map, rows -3 .. WB + 2
+constexpr int M2_OFF = M1_OFF + (WB16 + 8) * 4;
+static_assert(M2_OFF + (WB16 + 8) * 4 <= (int)h16c::LDS_BYTES, "CBAM scratch fits BUF1");
+
+struct Lane {             // this lane's (row, slot) items of the pointwise passes
+  int w, h, rb, q, c16;
+  __device__ __forceinline__ Lane() {
+    const int t = h16c::tid();
+    w = __builtin_amdgcn_readfirstlane(t >> 6);
+    h = w / h16c::RB;
+    rb = w % h16c::RB;
+    q = (t & 63) >> 4;
+    c16 = t & 15;
+  }
+  __device__ __forceinline__ int row(int n) const { return rb * h16c::RW + 16 * n + c16; }
+  __device__ __forceinline__ int slot() const { return 4 * h + q; }
+};
+// sum / max over the 16 lanes of a row by DPP (pair, quad, half-row mirror, row mirror): every lane
+// of the row ends with the row's value, one VALU op per step
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row_sum(float v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x141>(v);
+  return v + dpp<0x140>(v);
+}
+__device__ __forceinline__ float row_max(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  v = fmaxf(v, dpp<0x141>(v));
+  return fmaxf(v, dpp<0x140>(v));
+}
+// over lanes l, l ^ 16, l ^ 32, l ^ 48 (v_permlane32/16_swap)
+__device__ __forceinline__ float quarter_max(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float h = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(h), __float_as_uint(h), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+// per-channel sum / max of u (BUF0) over the tile's own positions and its edge rows -> slot (sc1);
+// arrive at the team counter
+__device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& ta, char* slot, unsigned* ctr,
+                                          bool arrive) {
+  char* lds = tl.lds;
+  const Lane ln;
+  const int tid = h16c::tid();
+  const int H = ta.halo, T = ta.T;
+  const int rend = H + min(T, tl.L - tl.base - H);
+  h16c::f32x8 sm = (h16c::f32x8)(0.f), mx = (h16c::f32x8)(-INFINITY);
+  const char* b0 = lds + h16c::BUF0 + (ln.h ? tl.koff[2][1] : tl.koff[2][0]);
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int r = ln.row(n);
+    if (r >= H && r < rend) {
+      const h16c::f32x8 u = __builtin_convertvector(*(const V*)(b0 + n * 16 * h16c::ROWB), h16c::f32x8);
+      sm += u;
+      mx = __builtin_elementwise_max(mx, u);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sm[j] = row_sum(sm[j]);
+    mx[j] = row_max(mx[j]);
+  }
+  float* rs = (float*)(lds + RED16_OFF);
+  unsigned* rm = (unsigned*)(lds + RED16_OFF + 4 * 64 * 4);
+  if (ln.c16 == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = h16_channel(ln.slot(), j);
+      rs[ln.rb * 64 + c] = sm[j];
+      rm[ln.rb * 64 + c] = f2ord(mx[j]);
+    }
+  }
+  __syncthreads();
+  // one store phase: the statistics (wave 0) and the edge rows (u, f16) for the neighbours (waves
+  // 1-2): block 0 = rows [2H - 5, 2H) (the left neighbour's rows [WB - 5, WB)), block 1 = rows
+  // [T, T + 5); every storing wave drains its stores, the workgroup barrier, then the arrival
+  if (tid < 64) {
+    const int c = tid;
+    double sv = 0.0;
+    unsigned m = 0;
+#pragma unroll
+    for (int k = 0; k < h16c::RB; ++k) {
+      sv += (double)rs[k * 64 + c];
+      m = max(m, rm[k * 64 + c]);
+    }
+    __hip_atomic_store((double*)slot + c, sv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((unsigned*)(slot + 512) + c, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (tid < 64 + 2 * EDGE_ROWS * 8) {
+    const int i = tid - 64, e = i / (EDGE_ROWS * 8), k = (i / 8) % EDGE_ROWS, g = i & 7;
+    const int r = e == 0 ? 2 * H - EDGE_ROWS + k : T + k;
+    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slot, 0, SLOT16_BYTES, 0x00020000);
+    const u32x4 v = *(const u32x4*)(lds + h16c::BUF0 + h16c::soff(r, g));
+    __builtin_amdgcn_raw_buffer_store_b128(v, sr, STAT_BYTES + e * EDGE16_BYTES + (k * 8 + g) * 16, 0, 16);
+  }
+  if (tid < 64 + 2 * EDGE_ROWS * 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0 && arrive) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// apply the CBAM whose statistics sit in the team's slots to u (BUF0): h = [identity +] u*ca*sa
+// [then ReLU], written over u; idv: the identity (LINEAR_SAVE layout) for res != RES_NONE
+__device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta, const char* slots0, int cbam_slot,
+                                        bool bias, int res, const V* idv, Stamps& st) {
+  char* lds = tl.lds;
+  const Lane ln;
+  const int tid = h16c::tid(), lane = tid & 63, w = ln.w;
+  const float* cw = tl.small + cbam_slot * SMALL_SLOT_FLOATS;      // fc.0.weight [4][64]
+  const float* cw2 = cw + SMALL_SLOT_FLOATS;                       // fc.2.weight [64][4]
+  const float* cmisc = cw2 + SMALL_SLOT_FLOATS;                    // fc.0.bias[4], fc.2.bias[64], sa.w[2][7], sa.b
+  const float cwv = cw[(w & 3) * 64 + lane];
+  const float b1 = bias ? cmisc[w & 3] : 0.f;
+  const f32x4 cw2v = *(const f32x4*)(cw2 + 4 * lane);
+  const float b2 = bias ? cmisc[4 + lane] : 0.f;
+  const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slots0, 0, ta.TT * SLOT16_BYTES, 0x00020000);
+
+  // halo refresh, fetched first: u of rows [0, 5) from the left neighbour's block 1, rows
+  // [WB - 5, WB) from the right neighbour's block 0 (first / last tile: no neighbour)
+  const int edge_e = tid / (EDGE_ROWS * 8), edge_k = (tid / 8) % EDGE_ROWS, edge_g = tid & 7;
+  bool has_edge = false;
+  u32x4 edge_u = {0u, 0u, 0u, 0u};
+  if (tid < 2 * EDGE_ROWS * 8) {
+    const int tile = (tl.base + ta.halo) / ta.T;
+    const int nb = edge_e == 0 ? tile - 1 : tile + 1;
+    if (nb >= 0 && nb < ta.TT) {
+      edge_u = __builtin_amdgcn_raw_buffer_load_b128(
+          sr, nb * SLOT16_BYTES + STAT_BYTES + (1 - edge_e) * EDGE16_BYTES + (edge_k * 8 + edge_g) * 16, 0, 16);
+      has_edge = true;
+    }
+  }
+  // the spectrum's per-channel mean and max over the TT slots, combined in a fixed order
+  double* pool = (double*)(lds + POOL_OFF);
+  {
+    const int c = tid & 63, part = tid >> 6;
+    double sp = 0.0;
+    unsigned mp = 0;
+    constexpr int PER = 4;
+    for (int t0 = part; t0 < ta.TT; t0 += h16c::WAVES * PER) {
+      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+      u32x2 sv[PER];
+      unsigned mv[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int t = t0 + h16c::WAVES * k;
+        const int off = (t < ta.TT ? t : 0) * SLOT16_BYTES;
+        sv[k] = __builtin_amdgcn_raw_buffer_load_b64(sr, off + 8 * c, 0, 16);
+        mv[k] = __builtin_amdgcn_raw_buffer_load_b32(sr, off + 512 + 4 * c, 0, 16);
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        if (t0 + h16c::WAVES * k < ta.TT) {
+          sp += __builtin_bit_cast(double, sv[k]);
+          mp = max(mp, mv[k]);
+        }
+      }
+    }
+    double* ps = (double*)(lds + SLP_OFF);
+    unsigned* pm = (unsigned*)(lds + SLP_OFF + 8 * 64 * 8);
+    ps[part * 64 + c] = sp;
+    pm[part * 64 + c] = mp;
+    __syncthreads();
+    if (tid < 64) {
+      double sum = 0.0;
+      unsigned m = 0;
+#pragma unroll
+      for (int k = 0; k < h16c::WAVES; ++k) {
+        sum += ps[k * 64 + tid];
+        m = max(m, pm[k * 64 + tid]);
+      }
+      pool[tid] = (double)(float)(sum / (double)tl.L);
+      pool[64 + tid] = (double)ord2f(m);
+    }
+  }
+  if (has_edge) {
+    const int r = edge_e == 0 ? edge_k : WB16 - EDGE_ROWS + edge_k;
+    *(u32x4*)(lds + h16c::BUF0 + h16c::soff(r, edge_g)) = edge_u;
+  }
+  __syncthreads();
+  st(10);
+  // channel attention: hidden unit (w & 3) of the shared MLP for the avg (w < 4) / max pooled vector
+  float* h1 = (float*)(lds + H1_16_OFF);
+  float* ca = (float*)(lds + CA16_OFF);
+  {
+    float a = cwv * (float)pool[(w >> 2) * 64 + lane];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    if (lane == 0) h1[w] = fmaxf(a + b1, 0.f);
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float oa = b2, om = b2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      oa = fmaf(cw2v[j], h1[j], oa);
+      om = fmaf(cw2v[j], h1[4 + j], om);
+    }
+    ca[tid] = sigm(oa + om);
+  }
+  __syncthreads();
+  st(11);
+
+  // spatial statistics of u*ca: per item 8 channels in packed f16 (the mode's storage precision:
+  // u is f16, ca rounds to f16), the partial sum / max to f32, the 4 quarters of a wave (32
+  // channels) by lane swaps, the two channel halves through LDS
+  char* b0 = lds + h16c::BUF0 + (ln.h ? tl.koff[2][1] : tl.koff[2][0]);
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  V cah;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cah[j] = (_Float16)ca[h16_channel(ln.slot(), j)];
+  float* s1h = (float*)(lds + S1H_OFF);
+  float* s2h = (float*)(lds + S2H_OFF);
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const V v = *(const V*)(b0 + n * 16 * h16c::ROWB) * cah;
+    const h2 s01 = __builtin_shufflevector(v, v, 0, 1) + __builtin_shufflevector(v, v, 2, 3);
+    const h2 s45 = __builtin_shufflevector(v, v, 4, 5) + __builtin_shufflevector(v, v, 6, 7);
+    const h2 m01 = __builtin_elementwise_max(__builtin_shufflevector(v, v, 0, 1), __builtin_shufflevector(v, v, 2, 3));
+    const h2 m45 = __builtin_elementwise_max(__builtin_shufflevector(v, v, 4, 5), __builtin_shufflevector(v, v, 6, 7));
+    const h2 ss = s01 + s45, mm = __builtin_elementwise_max(m01, m45);
+    float sm = (float)ss[0] + (float)ss[1];
+    float mx = fmaxf((float)mm[0], (float)mm[1]);
+    sm = quarter_sum(sm);
+    mx = quarter_max(mx);
+    if (ln.q == 0) {
+      s1h[ln.h * WB16 + ln.row(n)] = sm;
+      s2h[ln.h * WB16 + ln.row(n)] = mx;
+    }
+  }
+  __syncthreads();
+  st(12);
+  // the [mean; max] map over window rows -3 .. WB + 2 (index r + 3), zero outside the tile and [0, L)
+  float* m1 = (float*)(lds + M1_OFF);
+  float* m2 = (float*)(lds + M2_OFF);
+  for (int i = tid; i < WB16 + 6; i += h16c::THREADS) {
+    const int rr = i - 3, p = tl.base + rr;
+    const bool in = rr >= 0 && rr < WB16 && p >= 0 && p < tl.L;
+    m1[i] = in ? (s1h[rr] + s1h[WB16 + rr]) * (1.0f / 64.0f) : 0.f;
+    m2[i] = in ? fmaxf(s2h[rr], s2h[WB16 + rr]) : 0.f;
+  }
+  __syncthreads();
+  float* sa = (float*)(lds + SA16_OFF);
+  for (int r = tid; r < WB16; r += h16c::THREADS) {
+    float a = bias ? cmisc[82] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      a = fmaf(cmisc[68 + k], m1[r + k], a);
+      a = fmaf(cmisc[75 + k], m2[r + k], a);
+    }
+    sa[r] = sigm(a);
+  }
+  __syncthreads();
+  st(13);
+  // h = [identity +] u*ca*sa [relu], in place, packed f16; rows outside [0, L) zero
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int r = ln.row(n);
+    V* pu = (V*)(b0 + n * 16 * h16c::ROWB);
+    V hv = (*pu * cah) * (V)((_Float16)sa[r]);
+    if (res != RES_NONE) {
+      hv += idv[n];
+      if (res == RES_ADD_RELU) hv = __builtin_elementwise_max(hv, (V)((_Float16)0));
+    }
+    if (!h16c::in_range(tl.base + r, tl.L)) hv = (V)((_Float16)0);
+    *pu = hv;
+  }
+  __syncthreads();
+}
+
+template <bool ADS, bool EDGE>
+__device__ __forceinline__ void team16_spectra(char* lds, const uint8_t* blob, const uint8_t* big16, const float* x,
+                                               float* y, int L, const TeamArgs& ta, int team, int tile) {
+  unsigned* ctr = ta.counters + (size_t)team * TEAM_CTR_STRIDE;
+  char* tslots = ta.slots + (size_t)team * 2 * ta.TT * SLOT16_BYTES;
+  unsigned nbar = 0;
+  Stamps st;
+  st.init();
+  for (int64_t n = team; n < ta.n; n += ta.teams) {
+    h16c::Tile tl = h16c::init_tile(lds, blob, big16, x + (size_t)n * L, L, tile * ta.T - ta.halo);
+    h16c::Frags F0, F1;
+    V id[NT];
+    auto cbam = [&](int slot, int res) {
+      char* mine = tslots + ((size_t)(nbar & 1) * ta.TT + tile) * SLOT16_BYTES;
+      const bool skip = ta.force_miss > 0 && __builtin_amdgcn_workgroup_id_x() == 0 && nbar + 1 == (unsigned)ta.force_miss;
+      st(1);
+      publish16(tl, ta, mine, ctr, !skip);
+      st(3);
+      team_wait(ta, ctr, (nbar + 1) * (unsigned)ta.TT);
+      st(4);
+      apply16(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT16_BYTES, slot, ADS, res, id, st);
+      st(5);
+      ++nbar;
+    };
+    h16c::load_frags(tl, 0, F0);
+    h16c::stem(tl, 0, h16c::BUF0);
+    h16c::lds_barrier();
+    if (ADS) {
+      // ADSDN/train.py:160-167: cbam(relu(conv_ds x)); relu(conv1); relu(conv2); cbam;
+      // 15 x relu(cbam(bn2(conv2(relu(bn1(conv1 x))))) + x); conv_out
+      cbam(2, RES_NONE);
+      h16c::layer<h16c::RELU, EDGE>(tl, h16c::BUF0, h16c::BUF1, 1, F0, F1);
+      h16c::layer<h16c::RELU, EDGE>(tl, h16c::BUF1, h16c::BUF0, 1, F1, F0);
+      cbam(5, RES_NONE);
+      for (int b = 0; b < 15; ++b) {
+        h16c::layer<h16c::RELU, EDGE>(tl, h16c::BUF0, h16c::BUF1, 1, F0, F1);
+        h16c::layer<h16c::LINEAR_SAVE, EDGE>(tl, h16c::BUF1, h16c::BUF0, 1, F1, F0, true, id);
+        cbam(8 + 3 * b, RES_ADD_RELU);
+      }
+    } else {
+      // APIDN/train.py:150-159: h = relu(conv_ds x); 15 x x += cbam(bn(conv(relu(bn(conv x)))));
+      // sigmoid(conv_out(x + h))
+      for (int b = 0; b < 15; ++b) {
+        h16c::layer<h16c::RELU, EDGE>(tl, h16c::BUF0, h16c::BUF1, 1, F0, F1);
+        h16c::layer<h16c::LINEAR_SAVE, EDGE>(tl, h16c::BUF1, h16c::BUF0, 1, F1, F0, true, id);
+        cbam(2 + 3 * b, RES_ADD);
+      }
+      h16c::stem<true>(tl, 0, h16c::BUF0);       // + h, recomputed from x
+      h16c::lds_barrier();
+    }
+    float o[h16c::HN];
+    h16c::head<EDGE>(tl, h16c::BUF0, F0, F1, false, o);
+    const bool failed = __hip_atomic_load(ta.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+#pragma unroll
+    for (int k = 0; k < h16c::HN; ++k) {
+      if (!ADS) o[k] = sigm(o[k]);
+      if (failed) o[k] = __uint_as_float(0x7fc00000u);     // quiet NaN: an incomplete CBAM hand-off
+    }
+    h16c::store_out(tl, y, (int)n, o, ta.halo, ta.T);
+    __syncthreads();                 // the next spectrum's stem overwrites the rows the head read
+    st(6);
+  }
+  if (RDN_TEAM_STAMPS && __builtin_amdgcn_workitem_id_x() == 0 && ta.stamps)
+    for (int k = 0; k < NSTAMP; ++k) ta.stamps[(size_t)__builtin_amdgcn_workgroup_id_x() * NSTAMP + k] = st.acc[k];
+}
+}  // namespace t16
+
+template <bool ADS>
+__global__ __launch_bounds__(h16c::THREADS) void team16_forward(const uint8_t* __restrict__ blob,
+                                                                const uint8_t* __restrict__ big16,
+                                                                const float* __restrict__ x, float* __restrict__ y,
+                                                                int L, TeamArgs ta) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int team = __builtin_amdgcn_workgroup_id_x() / ta.TT, tile = __builtin_amdgcn_workgroup_id_x() - team * ta.TT;
+  const int base = tile * ta.T - ta.halo;
+  // a tile holds positions outside [0, L) for every spectrum or for none (one L per launch)
+  if (base >= 0 && base + t16::WB16 <= L) t16::team16_spectra<ADS, false>(lds, blob, big16, x, y, L, ta, team, tile);
+  else t16::team16_spectra<ADS, true>(lds, blob, big16, x, y, L, ta, team, tile);
+}
+
 }  // namespace cb
 
 // ---- host ----------------------------------------------------------------------------------------
@@ -848,45 +1241,59 @@ static team_kernel_t team_kernel(int arch, int mode) {
   if (mode == ip::MODE_F16) return ads ? team_forward<ip::MODE_F16, true> : team_forward<ip::MODE_F16, false>;
   return ads ? team_forward<ip::MODE_B1, true> : team_forward<ip::MODE_B1, false>;
 }
+// team kernel of RDN_F16 on the ping-pong engine (cb::team16_forward): its own team mode
+constexpr int MODE_P16 = 8;
+typedef void (*team16_kernel_t)(const uint8_t*, const uint8_t*, const float*, float*, int, cb::TeamArgs);
+static team16_kernel_t team16_kernel(int arch) {
+  return arch == ADSDN ? cb::team16_forward<true> : cb::team16_forward<false>;
+}
+size_t pp16_section_offset_arch(int arch);   // pack.cpp: the RDN_F16 blob's ping-pong section
 static int dtype_mode(int dtype) {
   return dtype == F32 ? ip::MODE_F32 : dtype == BF16X3 ? ip::MODE_X3 : dtype == F16F8 ? ip::MODE_H8
        : dtype == F16 ? ip::MODE_F16 : ip::MODE_B1;
 }
 // attribute slots 40-49 (team kernels) and 64-68 (segment kernels), host_util.hpp
-static int team_slot(int arch, int mode) { return 40 + 2 * mode + (arch == ADSDN); }
+static int team_slot(int arch, int mode) { return mode == MODE_P16 ? 80 + (arch == ADSDN) : 40 + 2 * mode + (arch == ADSDN); }
+static const void* team_fn(int arch, int mode) {
+  return mode == MODE_P16 ? (const void*)team16_kernel(arch) : (const void*)team_kernel(arch, mode);
+}
+static int team_lds(int mode) { return mode == MODE_P16 ? (int)h16c::LDS_BYTES : (int)cb::SEG_LDS_BYTES; }
+// the team kernel RDN_<dtype> runs (RDN_F16: the ping-pong one)
+static int team_mode(int dtype) { return dtype == F16 ? MODE_P16 : dtype_mode(dtype); }
 
 // co-resident workgroups per CU of the team kernel on `dev` (0 on any failure)
 static int team_blocks_per_cu(int arch, int mode, int dev) {
-  const team_kernel_t k = team_kernel(arch, mode);
-  if (ensure_dynamic_lds((const void*)k, team_slot(arch, mode), (int)cb::SEG_LDS_BYTES, dev) != hipSuccess) return 0;
+  const void* k = team_fn(arch, mode);
+  if (ensure_dynamic_lds(k, team_slot(arch, mode), team_lds(mode), dev) != hipSuccess) return 0;
   int cur = 0, nb = 0;
   if (hipGetDevice(&cur) != hipSuccess) return 0;
   if (cur != dev && hipSetDevice(dev) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k, THREADS, cb::SEG_LDS_BYTES) != hipSuccess) nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, THREADS, team_lds(mode)) != hipSuccess) nb = 0;
   if (cur != dev) (void)hipSetDevice(cur);
   return nb;
 }
 
 static TeamGeo team_geo(int arch, int mode, int64_t L, int dev) {
   TeamGeo g{};
+  const bool p16 = mode == MODE_P16;
   g.halo = cb::TEAM_HALO;                  // halos refreshed from the neighbours at every CBAM
-  g.T = WB - 2 * g.halo;
+  g.T = (p16 ? cb::t16::WB16 : WB) - 2 * g.halo;
   g.TT = (int)((L + g.T - 1) / g.T);
   const int resident = device_cus(dev) * team_blocks_per_cu(arch, mode, dev);
   g.teams = resident > 0 ? resident / g.TT : 0;
   const char* env = getenv("RDN_CBAM_SEGMENTS");       // diagnostics: force the per-segment path
   if (env && env[0] == '1') g.teams = 0;
   if (g.teams > 0) {
-    g.slots = (size_t)g.teams * 2 * g.TT * cb::SLOT_BYTES;
+    g.slots = (size_t)g.teams * 2 * g.TT * (p16 ? cb::t16::SLOT16_BYTES : cb::SLOT_BYTES);
     g.counters = (size_t)g.teams * cb::TEAM_CTR_STRIDE * 4;
-    g.hsave = (size_t)g.teams * g.TT * WB * 64 * 4;
+    g.hsave = p16 ? 0 : (size_t)g.teams * g.TT * WB * 64 * 4;     // p16: the identity lives in VGPRs
     g.total = g.slots + g.counters + g.hsave + 256 + 4 * 256 + cb::STAMP_BYTES;
   }
   return g;
 }
 
 size_t cbam_workspace_bytes(int arch, int dtype, int64_t n, int64_t L, hipStream_t stream) {
-  const TeamGeo g = team_geo(arch, dtype_mode(dtype), L, stream_device(stream));
+  const TeamGeo g = team_geo(arch, team_mode(dtype), L, stream_device(stream));
   if (g.teams > 0) return g.total;
   const int64_t c = n < CBAM_CHUNK ? n : CBAM_CHUNK;
   return 4 * act_bytes(c, L) + 2 * (size_t)c * 64 * (sizeof(double) + sizeof(unsigned)) + 256;
@@ -903,8 +1310,7 @@ static unsigned* team_err(const TeamGeo& g, void* ws) { return (unsigned*)(team_
 static hipError_t launch_team(int arch, int mode, const TeamGeo& g, const uint8_t* blob, const float* x, float* y,
                               int64_t n, int L, void* ws, hipStream_t stream) {
   using namespace cb;
-  const team_kernel_t k = team_kernel(arch, mode);
-  const hipError_t ea = ensure_dynamic_lds((const void*)k, team_slot(arch, mode), (int)SEG_LDS_BYTES, stream_device(stream));
+  const hipError_t ea = ensure_dynamic_lds(team_fn(arch, mode), team_slot(arch, mode), team_lds(mode), stream_device(stream));
   if (ea != hipSuccess) return ea;
   char* base = team_base(ws);
   TeamArgs ta{};
@@ -926,7 +1332,14 @@ static hipError_t launch_team(int arch, int mode, const TeamGeo& g, const uint8_
   if (e != hipSuccess) return e;
   const int64_t teams = n < g.teams ? n : g.teams;    // never more teams than spectra
   ta.teams = (int)teams;
-  hipLaunchKernelGGL(k, dim3((unsigned)(teams * g.TT)), dim3(THREADS), SEG_LDS_BYTES, stream, blob, x, y, L, ta);
+  if (mode == MODE_P16) {
+    const uint8_t* big16 = blob + pp16_section_offset_arch(arch);
+    hipLaunchKernelGGL(team16_kernel(arch), dim3((unsigned)(teams * g.TT)), dim3(THREADS), (uint32_t)team_lds(mode),
+                       stream, blob, big16, x, y, L, ta);
+  } else {
+    hipLaunchKernelGGL(team_kernel(arch, mode), dim3((unsigned)(teams * g.TT)), dim3(THREADS), SEG_LDS_BYTES, stream,
+                       blob, x, y, L, ta);
+  }
   return hipGetLastError();
 }
 
@@ -943,10 +1356,11 @@ hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const f
   const int dev = stream_device(stream);
   const hipError_t ea = ensure_dynamic_lds((const void*)k, 64 + mode, (int)SEG_LDS_BYTES, dev);
   if (ea != hipSuccess) return ea;
-  const TeamGeo tg = team_geo(arch, mode, L, dev);
+  const int tmode = team_mode(dtype);
+  const TeamGeo tg = team_geo(arch, tmode, L, dev);
   if (tg.teams > 0) {
     if (ws_bytes < tg.total) return hipErrorInvalidValue;
-    return launch_team(arch, mode, tg, blob, x, y, n, L, ws, stream);
+    return launch_team(arch, tmode, tg, blob, x, y, n, L, ws, stream);
   }
   const bool adsdn = arch == ADSDN;
   const int64_t chunk = n < CBAM_CHUNK ? n : CBAM_CHUNK;
@@ -1021,7 +1435,7 @@ hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes
   *timed_out = 0;
   hipError_t e = hipStreamSynchronize(stream);
   if (e != hipSuccess) return e;
-  const TeamGeo tg = team_geo(arch, dtype_mode(dtype), L, stream_device(stream));
+  const TeamGeo tg = team_geo(arch, team_mode(dtype), L, stream_device(stream));
   if (tg.teams <= 0 || !ws || ws_bytes < tg.total) return hipSuccess;   // segment path: no hand-off
   unsigned err = 0;
   e = hipMemcpy(&err, team_err(tg, ws), sizeof(err), hipMemcpyDeviceToHost);

@@ -307,6 +307,8 @@ enum Epi : int {
   RELU = 0,       // relu(acc + b)
   LINEAR = 1,     // acc + b                (PIDN block output: BN without ReLU)
   RES_RELU = 2,   // relu(acc + b + dst)    (DSDN ResidualBlock: out += identity; relu)
+  LINEAR_SAVE = 3,  // acc + b, the dst slot's previous content saved to idv[n] first (the CBAM
+                    // networks' ResidualBlock identity, held in VGPRs across the CBAM: cbam.hip)
 };
 
 // LDS byte addresses of this lane's B fragment for k-step s = (tap t, part u) of N-tile n, from
@@ -349,7 +351,8 @@ static_assert(RDN_H16_LDSTEP * (NLOAD - 1) < KS * NT, "every operand load of the
 // G (header).
 template <int EPI, bool EDGE>
 __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int dil, const Frags& F, Frags& G,
-                                      bool has_next = true) {
+                                      bool has_next = true, V* idv = nullptr) {
+  static_assert(EPI != LINEAR_SAVE || !RDN_H16_M32, "LINEAR_SAVE: one slot per N-tile");
   const int lane = tid() & 63, w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB;
   const int next = tl.layer + 1;
   asm volatile("" : "+s"(src), "+s"(dst));   // per-layer addresses: not hoisted out of a network's loop (spills)
@@ -363,6 +366,10 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   // MFMA pipe to itself.  It still fetches the next layer's operands and meets the barrier.
   if (EDGE && pos0 >= tl.L + 2) {
     if (has_next) load_frags(tl, next, G);
+    if constexpr (EPI == LINEAR_SAVE) {
+#pragma unroll
+      for (int n = 0; n < NT; ++n) idv[n] = (V)((E)0);
+    }
     tl.layer += 1;
     lds_barrier();
     return;
@@ -376,14 +383,14 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     // ReLU after the rounding, on packed f16 (4 v_pk_max_f16 instead of 8 v_max_f32; the rounding is
     // monotone, so max(f16(v), 0) = f16(max(v, 0)) up to the sign of a zero)
     V hv = __builtin_convertvector(v, V);
-    if (EPI != LINEAR) hv = __builtin_elementwise_max(hv, (V)((E)0));
+    if (EPI != LINEAR && EPI != LINEAR_SAVE) hv = __builtin_elementwise_max(hv, (V)((E)0));
     if (EDGE && !valid) hv = (V)((E)0);
 #if defined(RDN_ABLATE_NOSTORE)            // diagnostic builds only (tools/ablate.py)
     if (hv[0] == (E)1234.f)
 #endif
     *p = hv;
 #else
-    if (EPI != LINEAR) v = __builtin_elementwise_max(v, (f32x8)(0.f));
+    if (EPI != LINEAR && EPI != LINEAR_SAVE) v = __builtin_elementwise_max(v, (f32x8)(0.f));
     if (EDGE && !valid) v = (f32x8)(0.f);
 #if defined(RDN_ABLATE_NOSTORE)
     if (v[0] == 123456.f)
@@ -404,7 +411,9 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   const int sa = (int)dst + (h ? tl.koff[2][1] : tl.koff[2][0]);     // slot 4h + q of row r0
   auto epilogue = [&](int n, const Acc& a) {
     const bool valid = !EDGE || in_range(pos0 + NR * n + (lane & 15), tl.L);
-    store_slot((V*)(tl.lds + sa + n * NR * ROWB), __builtin_shufflevector(a.v[0], a.v[1], 0, 1, 2, 3, 4, 5, 6, 7), valid);
+    V* p = (V*)(tl.lds + sa + n * NR * ROWB);
+    if constexpr (EPI == LINEAR_SAVE) idv[n] = *p;
+    store_slot(p, __builtin_shufflevector(a.v[0], a.v[1], 0, 1, 2, 3, 4, 5, 6, 7), valid);
   };
 #endif
 
@@ -502,17 +511,16 @@ __device__ __forceinline__ void head(Tile& tl, uint32_t src, const Frags& F, Fra
   tl.layer += 1;
 }
 
-__device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const float* x, int L, int T, int tiles,
-                                          int halo, int& n_out) {
-  const int n = __builtin_amdgcn_workgroup_id_x() / tiles, tile = __builtin_amdgcn_workgroup_id_x() - n * tiles;
-  n_out = n;
+// tile over positions [base, base + WB) of the spectrum at x; big: the blob's big-layer section
+__device__ __forceinline__ Tile init_tile(char* lds, const uint8_t* blob, const uint8_t* big, const float* x, int L,
+                                          int base) {
   Tile tl;
   tl.lds = lds;
-  tl.x = x + (size_t)n * L;
+  tl.x = x;
   tl.L = L;
-  tl.base = tile * T - halo;
+  tl.base = base;
   tl.small = (const float*)blob;
-  tl.big = blob + SMALL_BYTES;
+  tl.big = big;
   // raw buffer over the big-layer section (stride 0, 2 GiB bound; dword 3 = 0x00020000, the raw
   // 32-bit data format of the gfx9 buffer descriptor)
   tl.wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)tl.big, 0, 0x7fffffff, 0x00020000);
@@ -534,6 +542,13 @@ __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const 
     for (int u = 0; u < 2; ++u) tl.koff[d + 2][u] = soff(tl.r0 + d, 4 * u + q);
 #endif
   return tl;
+}
+
+__device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const float* x, int L, int T, int tiles,
+                                          int halo, int& n_out) {
+  const int n = __builtin_amdgcn_workgroup_id_x() / tiles, tile = __builtin_amdgcn_workgroup_id_x() - n * tiles;
+  n_out = n;
+  return init_tile(lds, blob, blob + SMALL_BYTES, x + (size_t)n * L, L, tile * T - halo);
 }
 
 // tile row of head output j of this lane (lanes 0..HEAD_LANES-1); a row no tile owns (WB) for the

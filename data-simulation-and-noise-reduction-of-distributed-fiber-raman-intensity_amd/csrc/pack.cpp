@@ -208,11 +208,31 @@ static uint16_t to_bf16(double v) {      // fp64 -> fp32 -> bf16, round to neare
   return (uint16_t)(u >> 16);
 }
 
-static uint16_t to_f16(double v) {       // fp64 -> fp32 -> f16, round to nearest even
-  const _Float16 h = (_Float16)(float)v;
-  uint16_t u;
-  std::memcpy(&u, &h, 2);
-  return u;
+// fp64 -> fp32 -> f16, each step round to nearest even.  The f16 step is integer arithmetic on the
+// fp32 bits: the host's _Float16 conversion differed by one ulp near ties between the -O3 library
+// and the -O1 sanitizer build of the same source (tests/test_abi.py test_host_sanitizer_pack)
+static uint16_t to_f16(double v) {
+  const float f = (float)v;
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint32_t sign = (x >> 16) & 0x8000u, mant = x & 0x7fffffu;
+  const int exp = (int)((x >> 23) & 0xffu);
+  if (exp == 0xff) return (uint16_t)(sign | 0x7c00u | (mant ? 0x200u : 0u));    // inf / nan
+  const int e = exp - 127 + 15;                                                  // f16 biased exponent
+  if (e >= 31) return (uint16_t)(sign | 0x7c00u);                                // overflow
+  if (e <= 0) {                                                                  // f16 subnormal / zero
+    if (e < -10) return (uint16_t)sign;
+    const uint32_t m = mant | 0x800000u;
+    const int sh = 14 - e;
+    uint32_t h = m >> sh;
+    const uint32_t rem = m & ((1u << sh) - 1u), half = 1u << (sh - 1);
+    if (rem > half || (rem == half && (h & 1u))) ++h;
+    return (uint16_t)(sign | h);
+  }
+  uint32_t h = ((uint32_t)e << 10) | (mant >> 13);
+  const uint32_t rem = mant & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;                         // a carry rounds into the exponent
+  return (uint16_t)(sign | h);
 }
 
 static double from16(uint16_t u, bool f16) {
@@ -327,14 +347,14 @@ static int e8m0_for(double amax) {
 }
 
 static void pack_big_h8(const Folded& f, uint8_t* dst) {
-  _Float16* main = (_Float16*)dst;
+  uint16_t* main = (uint16_t*)dst;
   // hi / lo split of every weight: hi = f16(fp32(W)), lo = W - hi (fp64)
   std::vector<double> hi((size_t)C * C * 3), lo((size_t)C * C * 3);
   for (int co = 0; co < C; ++co)
     for (int ci = 0; ci < C; ++ci)
       for (int t = 0; t < 3; ++t) {
         const double w = co < f.cout ? f.W(co, ci, t) : 0.0;
-        const double h = (double)(_Float16)(float)w;
+        const double h = from16(to_f16(w), true);
         hi[((size_t)co * C + ci) * 3 + t] = h;
         lo[((size_t)co * C + ci) * 3 + t] = w - h;
       }
@@ -346,7 +366,7 @@ static void pack_big_h8(const Folded& f, uint8_t* dst) {
         for (int j = 0; j < 8; ++j) {
           const int t = s >> 1, u = s & 1;
           const int co = 16 * m + (lane & 15), ci = h16_channel(4 * u + (lane >> 4), j);
-          main[(((m * 6 + s) * 64) + lane) * 8 + j] = (_Float16)H(co, ci, t);
+          main[(((m * 6 + s) * 64) + lane) * 8 + j] = to_f16(H(co, ci, t));     // exact: H is an f16 value
         }
   // e4m3 activation byte b of a plane holds channel h16_channel(b >> 3, b & 7); blocks of 32 bytes
   // = channels [0, 32) and [32, 64)
@@ -438,8 +458,21 @@ static size_t layer_bytes(int layout) {
   return layout == BF16 || layout == F16 ? BIG_BYTES_BF16 : layout == F16F8 ? BIG_BYTES_H8 : BIG_BYTES_F32;
 }
 
-size_t packed_bytes(const std::vector<Op>& spec, int dtype) {
+// RDN_F16 on the CBAM networks: the in-place single-plane records (F16X: the per-segment kernels,
+// for spectra longer than the co-resident teams hold) are followed by a ping-pong section (fused16
+// layout, f16 fragments in h16_channel order, the head as its last record) for the team kernel
+// cb::team16_forward
+bool has_pp16_section(const std::vector<Op>& spec, int dtype) { return dtype == F16 && has_cbam(spec); }
+size_t pp16_section_offset(const std::vector<Op>& spec, int dtype) {
   return SMALL_BYTES + (size_t)big_layers(spec, dtype) * layer_bytes(big_layout(spec, dtype));
+}
+
+size_t pp16_section_offset_arch(int arch) { return pp16_section_offset(net_spec(arch), F16); }
+
+size_t packed_bytes(const std::vector<Op>& spec, int dtype) {
+  size_t n = SMALL_BYTES + (size_t)big_layers(spec, dtype) * layer_bytes(big_layout(spec, dtype));
+  if (has_pp16_section(spec, dtype)) n += (size_t)big_layers(spec, F16) * BIG_BYTES_BF16 + BIG_BYTES_BF16;
+  return n;
 }
 
 
@@ -489,6 +522,34 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
     }
   }
   if (rd.i != n) return "too many tensors: consumed " + std::to_string(rd.i) + " of " + std::to_string(n);
+  if (has_pp16_section(spec, dtype)) {        // second pass: the ping-pong records (BIG, then the head)
+    uint8_t* pp = out + pp16_section_offset(spec, dtype);
+    Reader r2{tensors, numels, n};
+    int k = 0;
+    for (const Op& o : spec) {
+      Folded f;
+      switch (o.kind) {
+        case OpKind::STEM:
+          if (!fold(r2, o, 1, C, f)) return r2.err;
+          break;
+        case OpKind::BIG:
+          if (!fold(r2, o, C, C, f)) return r2.err;
+          pack_big_bf16(f, pp + (size_t)(k++) * BIG_BYTES_BF16, true);
+          break;
+        case OpKind::HEAD:
+          if (!fold(r2, o, C, 1, f)) return r2.err;
+          pack_big_bf16(f, pp + (size_t)(k++) * BIG_BYTES_BF16, true);
+          break;
+        case OpKind::CBAM: {
+          std::vector<float> scratch(3 * SMALL_SLOT_FLOATS);
+          Op o2 = o;
+          o2.slot = 0;
+          if (!pack_cbam(r2, o2, scratch.data())) return r2.err;
+          break;
+        }
+      }
+    }
+  }
   if (dtype == F16F8 || dtype == F16MIX) set_corr_mask(out, dtype == F16F8 ? ~0ull : f16mix_default_mask(arch));
   return "";
 }

@@ -256,12 +256,45 @@ def test_pack_layout_f16mix_head_record():
     assert bias[0] == b[0] and bias[32] == b[0] and np.count_nonzero(bias) <= 2
 
 
+@pytest.mark.parametrize("arch,nbig", [("ADSDN", 32), ("APIDN", 30)])
+def test_pack_layout_cbam_f16_pingpong_section(arch, nbig):
+    """RDN_F16 on the CBAM networks: the in-place single-plane records (per-segment kernels) are followed
+    by a ping-pong section for the team kernel (cbam.hip team16_forward): one fused16 record per big layer
+    (f16 fragments in h16_channel K order, bias at 24576) and the head (conv_out) as the last record."""
+    from raman_mi355x import engine
+    sd = golden_state_dict(arch, "trained")
+    blob = engine.pack(arch, sd, "f16", "cpu").numpy()
+    off = SMALL + nbig * 49408
+    assert blob.size == engine.packed_size(arch, "f16") == off + (nbig + 1) * 24832
+    lane = np.arange(64)
+    # big layer 2 (the first ResidualBlock's / block's first conv, BN folded)
+    conv, bn = ("res_blocks.0.conv1", "res_blocks.0.bn1") if arch == "ADSDN" else ("res_blocks.1.0", "res_blocks.1.1")
+    k = 2
+    w, b = _fold(sd, conv, bn)
+    R = blob[off + k * 24832:off + (k + 1) * 24832]
+    frag = R[:24576].view(np.float16).reshape(4, 6, 64, 8)
+    for m in range(4):
+        for s_ in range(6):
+            t, u = s_ >> 1, s_ & 1
+            for j in range(8):
+                cin = 32 * u + 4 * (lane >> 4) + (j & 3) + 16 * (j >> 2)
+                np.testing.assert_array_equal(frag[m, s_, :, j], w[16 * m + (lane & 15), cin, t].astype(np.float16))
+    np.testing.assert_array_equal(R[24576:].view(np.float32), b.astype(np.float32))
+    # the head record: cout 0 in rows 0 and 32, bias copies at 0 and 32
+    wh, bh = _fold(sd, "conv_out" if arch == "ADSDN" else "conv_out.0", None)
+    H = blob[off + nbig * 24832:]
+    hf = H[:24576].view(np.float16).reshape(4, 6, 64, 8)
+    np.testing.assert_array_equal(hf[0, 0, 0, :4], wh[0, [0, 1, 2, 3], 0].astype(np.float16))
+    hb = H[24576:].view(np.float32)
+    assert hb[0] == bh[0] and hb[32] == bh[0]
+
+
 def _fold_f64(sd, conv):
     return sd[conv + ".weight"].double().numpy()
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("arch,dtype", [("RRCDNet", "f16f8"), ("RRCDNet", "f16mix"), ("ADSDN", "fp32"), ("DSDN", "bf16x3"),
+@pytest.mark.parametrize("arch,dtype", [("RRCDNet", "f16f8"), ("RRCDNet", "f16mix"), ("ADSDN", "f16"), ("ADSDN", "fp32"), ("DSDN", "bf16x3"),
                                         ("APIDN", "bf16-unsafe"), ("DenoiseCNN", "f16f8")])
 def test_host_sanitizer_pack(arch, dtype, tmp_path):
     """pack.cpp + abi.cpp built with ASan + UBSan (csrc/Makefile `asan`): packing a

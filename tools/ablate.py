@@ -28,7 +28,8 @@ VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "mixold": "-DRDN_F16MIX_HYBRID=0", "pkrelu0": "-DRDN_H16_PKRELU=0", "ld2": "-DRDN_H16_LDSTEP=2", "ld4": "-DRDN_H16_LDSTEP=4", "m32": "-DRDN_H16_M32=1",
             "m32ld2": "-DRDN_H16_M32=1 -DRDN_H16_LDSTEP=2", "m32pf2": "-DRDN_H16_M32=1 -DRDN_H16_PF=2",
             "ord": "-DRDN_H16_LDORDER=1", "ordld3": "-DRDN_H16_LDORDER=1 -DRDN_H16_LDSTEP=3", "ordld2": "-DRDN_H16_LDORDER=1 -DRDN_H16_LDSTEP=2",
-            "wsame": "-DRDN_ABLATE_WSAME", "whalf": "-DRDN_ABLATE_WHALF"}
+            "wsame": "-DRDN_ABLATE_WSAME", "whalf": "-DRDN_ABLATE_WHALF",
+            "sleep1": "-DRDN_TEAM_SLEEP=1", "sleep2": "-DRDN_TEAM_SLEEP=2"}
 
 
 def build():
@@ -117,14 +118,20 @@ def run():
         packed = {name: pack_with(lib, code) for name, lib in libs.items()}
         times = {k: [] for k in libs}
         outs = {}
+        wss = {}
+        for name, lib in libs.items():          # CBAM networks: the team kernel's workspace
+            wsz = ctypes.c_size_t()
+            assert lib.rdn_workspace_size(aid, code, B, L, ctypes.byref(wsz)) == 0
+            wss[name] = (torch.zeros(max(1, wsz.value), dtype=torch.uint8, device=dev), wsz.value)
         for rnd in range(4):
             for name, lib in libs.items():
                 stream = torch.cuda.current_stream().cuda_stream
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                lib.rdn_forward(aid, code, packed[name].data_ptr(), x.data_ptr(), y.data_ptr(), B, L, None, 0, stream)
+                wsp, wsn = wss[name][0].data_ptr(), wss[name][1]
+                lib.rdn_forward(aid, code, packed[name].data_ptr(), x.data_ptr(), y.data_ptr(), B, L, wsp, wsn, stream)
                 e0.record()
                 for _ in range(3):
-                    rc = lib.rdn_forward(aid, code, packed[name].data_ptr(), x.data_ptr(), y.data_ptr(), B, L, None, 0, stream)
+                    rc = lib.rdn_forward(aid, code, packed[name].data_ptr(), x.data_ptr(), y.data_ptr(), B, L, wsp, wsn, stream)
                     assert rc == 0, lib.rdn_last_error()
                 e1.record()
                 torch.cuda.synchronize()
