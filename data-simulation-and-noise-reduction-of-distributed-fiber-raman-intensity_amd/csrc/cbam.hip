@@ -858,9 +858,8 @@ constexpr int SC = h16c::BUF1;
 constexpr int RED16_OFF = SC;                                  // [4 row blocks][64] f32 sums, then u32 maxima
 constexpr int SLP_OFF = RED16_OFF + 2 * 4 * 64 * 4;            // [8 waves][64] f64 slot partials, then u32
 constexpr int POOL_OFF = SLP_OFF + 8 * 64 * 12;                // [2][64] f64: pooled avg / max
-constexpr int H1_16_OFF = POOL_OFF + 2 * 64 * 8;               // MLP hidden (8 f32)
-constexpr int CA16_OFF = H1_16_OFF + 64;                       // channel attention (64 f32)
-constexpr int S1H_OFF = CA16_OFF + 64 * 4;                     // [2 halves][WB16] partial sums over 32 channels
+constexpr int CA16_OFF = POOL_OFF + 2 * 64 * 8;                // channel attention, one copy per wave (8 x 64 f32)
+constexpr int S1H_OFF = CA16_OFF + 8 * 64 * 4;                 // [2 halves][WB16] partial sums over 32 channels
 constexpr int S2H_OFF = S1H_OFF + 2 * WB16 * 4;                // [2 halves][WB16] partial maxima
 constexpr int SA16_OFF = S2H_OFF + 2 * WB16 * 4;               // spatial attention per tile row
 constexpr int M1_OFF = SA16_OFF + WB16 * 4;                    // [mean_c; max_c] map, rows -3 .. WB + 2
@@ -917,11 +916,14 @@ __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& 
   const int rend = H + min(T, tl.L - tl.base - H);
   h16c::f32x8 sm = (h16c::f32x8)(0.f), mx = (h16c::f32x8)(-INFINITY);
   const char* b0 = lds + h16c::BUF0 + (ln.h ? tl.koff[2][1] : tl.koff[2][0]);
+  V uv[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) uv[n] = *(const V*)(b0 + n * 16 * h16c::ROWB);
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     const int r = ln.row(n);
     if (r >= H && r < rend) {
-      const h16c::f32x8 u = __builtin_convertvector(*(const V*)(b0 + n * 16 * h16c::ROWB), h16c::f32x8);
+      const h16c::f32x8 u = __builtin_convertvector(uv[n], h16c::f32x8);
       sm += u;
       mx = __builtin_elementwise_max(mx, u);
     }
@@ -978,8 +980,9 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   const float* cw = tl.small + cbam_slot * SMALL_SLOT_FLOATS;      // fc.0.weight [4][64]
   const float* cw2 = cw + SMALL_SLOT_FLOATS;                       // fc.2.weight [64][4]
   const float* cmisc = cw2 + SMALL_SLOT_FLOATS;                    // fc.0.bias[4], fc.2.bias[64], sa.w[2][7], sa.b
-  const float cwv = cw[(w & 3) * 64 + lane];
-  const float b1 = bias ? cmisc[w & 3] : 0.f;
+  f32x4 w1v;                                                       // fc.0 column `lane` (4 hidden units)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w1v[j] = cw[j * 64 + lane];
   const f32x4 cw2v = *(const f32x4*)(cw2 + 4 * lane);
   const float b2 = bias ? cmisc[4 + lane] : 0.f;
   const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slots0, 0, ta.TT * SLOT16_BYTES, 0x00020000);
@@ -1028,18 +1031,6 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
     unsigned* pm = (unsigned*)(lds + SLP_OFF + 8 * 64 * 8);
     ps[part * 64 + c] = sp;
     pm[part * 64 + c] = mp;
-    __syncthreads();
-    if (tid < 64) {
-      double sum = 0.0;
-      unsigned m = 0;
-#pragma unroll
-      for (int k = 0; k < h16c::WAVES; ++k) {
-        sum += ps[k * 64 + tid];
-        m = max(m, pm[k * 64 + tid]);
-      }
-      pool[tid] = (double)(float)(sum / (double)tl.L);
-      pool[64 + tid] = (double)ord2f(m);
-    }
   }
   if (has_edge) {
     const int r = edge_e == 0 ? edge_k : WB16 - EDGE_ROWS + edge_k;
@@ -1047,26 +1038,34 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   }
   __syncthreads();
   st(10);
-  // channel attention: hidden unit (w & 3) of the shared MLP for the avg (w < 4) / max pooled vector
-  float* h1 = (float*)(lds + H1_16_OFF);
-  float* ca = (float*)(lds + CA16_OFF);
+  // channel attention, evaluated whole by every wave (no barrier): the pooled avg / max of channel
+  // `lane` from the 8 partials in a fixed order, the 4 + 4 hidden units as sums over the 64 lanes
+  float cav;
   {
-    float a = cwv * (float)pool[(w >> 2) * 64 + lane];
+    const double* ps = (const double*)(lds + SLP_OFF);
+    const unsigned* pm = (const unsigned*)(lds + SLP_OFF + 8 * 64 * 8);
+    double sum = 0.0;
+    unsigned m = 0;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-    if (lane == 0) h1[w] = fmaxf(a + b1, 0.f);
-  }
-  __syncthreads();
-  if (tid < 64) {
+    for (int k = 0; k < h16c::WAVES; ++k) {
+      sum += ps[k * 64 + lane];
+      m = max(m, pm[k * 64 + lane]);
+    }
+    const float pa = (float)(sum / (double)tl.L), px = ord2f(m);
     float oa = b2, om = b2;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      oa = fmaf(cw2v[j], h1[j], oa);
-      om = fmaf(cw2v[j], h1[4 + j], om);
+      const float b1 = bias ? cmisc[j] : 0.f;
+      const float ha = fmaxf(quarter_sum(row_sum(w1v[j] * pa)) + b1, 0.f);
+      const float hm = fmaxf(quarter_sum(row_sum(w1v[j] * px)) + b1, 0.f);
+      oa = fmaf(cw2v[j], ha, oa);
+      om = fmaf(cw2v[j], hm, om);
     }
-    ca[tid] = sigm(oa + om);
+    cav = sigm(oa + om);
   }
-  __syncthreads();
+  // this lane's 8 channels of ca through the wave's own LDS row (in-order within a wave)
+  float* caw = (float*)(lds + CA16_OFF) + 64 * w;
+  caw[lane] = cav;
   st(11);
 
   // spatial statistics of u*ca: per item 8 channels in packed f16 (the mode's storage precision:
@@ -1076,12 +1075,15 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   typedef _Float16 h2 __attribute__((ext_vector_type(2)));
   V cah;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) cah[j] = (_Float16)ca[h16_channel(ln.slot(), j)];
+  for (int j = 0; j < 8; ++j) cah[j] = (_Float16)caw[h16_channel(ln.slot(), j)];
   float* s1h = (float*)(lds + S1H_OFF);
   float* s2h = (float*)(lds + S2H_OFF);
+  V uv[NT];                  // all reads first: one LDS round trip for the pass, not one per item
+#pragma unroll
+  for (int n = 0; n < NT; ++n) uv[n] = *(const V*)(b0 + n * 16 * h16c::ROWB);
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
-    const V v = *(const V*)(b0 + n * 16 * h16c::ROWB) * cah;
+    const V v = uv[n] * cah;
     const h2 s01 = __builtin_shufflevector(v, v, 0, 1) + __builtin_shufflevector(v, v, 2, 3);
     const h2 s45 = __builtin_shufflevector(v, v, 4, 5) + __builtin_shufflevector(v, v, 6, 7);
     const h2 m01 = __builtin_elementwise_max(__builtin_shufflevector(v, v, 0, 1), __builtin_shufflevector(v, v, 2, 3));
@@ -1121,11 +1123,17 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   __syncthreads();
   st(13);
   // h = [identity +] u*ca*sa [relu], in place, packed f16; rows outside [0, L) zero
+  float sv[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    uv[n] = *(const V*)(b0 + n * 16 * h16c::ROWB);
+    sv[n] = sa[ln.row(n)];
+  }
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     const int r = ln.row(n);
     V* pu = (V*)(b0 + n * 16 * h16c::ROWB);
-    V hv = (*pu * cah) * (V)((_Float16)sa[r]);
+    V hv = (uv[n] * cah) * (V)((_Float16)sv[n]);
     if (res != RES_NONE) {
       hv += idv[n];
       if (res == RES_ADD_RELU) hv = __builtin_elementwise_max(hv, (V)((_Float16)0));

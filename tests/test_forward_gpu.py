@@ -165,20 +165,21 @@ def test_cbam_team_halo_exchange(arch, L, dtype):
     assert err <= tol, f"{arch} L={L} {dtype}: {err:.3e} > {tol:.3e}"
 
 
+@pytest.mark.parametrize("dtype", ["f16f8", "f16"])
 @pytest.mark.parametrize("arch", ["ADSDN", "APIDN"])
-def test_cbam_team_timeout_is_reported(arch, monkeypatch):
+def test_cbam_team_timeout_is_reported(arch, dtype, monkeypatch):
     """A team member that never arrives at a CBAM hand-off (RDN_CBAM_FORCE_MISS=k: workgroup 0 skips
     its k-th arrival) must not yield plausible outputs with RDN_OK: rdn_forward_status reports
     RDN_EHIP, the module raises, and the affected spectra are NaN."""
     import raman_mi355x as R
     from raman_mi355x import _lib, engine
-    m = _model(arch, "synth", "f16f8")
+    m = _model(arch, "synth", dtype)
     x = torch.from_numpy(np.random.default_rng(5).uniform(0, 1, (2, 1, 1200)).astype(np.float32)).cuda()
     monkeypatch.setenv("RDN_CBAM_FORCE_MISS", "3")
     with pytest.raises(_lib.EngineError, match="timed out"):
         with torch.no_grad():
             m(x)
-    y = engine.forward(arch, "f16f8", m.packed_weights(x.device), x, check=False)
+    y = engine.forward(arch, dtype, m.packed_weights(x.device), x, check=False)
     torch.cuda.synchronize()
     assert torch.isnan(y[0]).any()
     monkeypatch.delenv("RDN_CBAM_FORCE_MISS")
@@ -199,6 +200,21 @@ def test_cbam_team_matches_segment_path(arch, monkeypatch):
     monkeypatch.delenv("RDN_CBAM_SEGMENTS")
     scale = max(np.abs(y_seg).max(), 1e-30)
     assert np.abs(y_team - y_seg).max() <= 2e-6 * scale, np.abs(y_team - y_seg).max() / scale
+
+
+@pytest.mark.parametrize("arch", ["ADSDN", "APIDN"])
+def test_cbam_team16_matches_segment_path(arch, monkeypatch):
+    """RDN_F16: the ping-pong team kernel (cbam.hip team16_forward) and the in-place per-segment launches
+    (RDN_CBAM_SEGMENTS=1) read different sections of the same blob and round differently (f16 storage in
+    both); they agree within the 16-bit bar, on a length that spans several 628-position tiles."""
+    m = _model(arch, "trained", "f16")
+    x = np.random.default_rng(4).uniform(0, 1, (3, 2600)).astype(np.float32)
+    y_team = _run(m, x)
+    monkeypatch.setenv("RDN_CBAM_SEGMENTS", "1")
+    y_seg = _run(m, x)
+    monkeypatch.delenv("RDN_CBAM_SEGMENTS")
+    assert np.isfinite(y_team).all()
+    assert np.abs(y_team - y_seg).max() <= BF16_ABS * max(1.0, float(np.abs(y_seg).max()))
 
 
 # halo rows per side of the 640-row fused tiles (csrc/common.hpp fused_halo)
