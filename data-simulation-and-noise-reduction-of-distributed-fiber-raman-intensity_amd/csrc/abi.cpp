@@ -1,6 +1,7 @@
 // C ABI (include/raman_mi355x.h): argument checking, error reporting and dispatch.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <string>
@@ -8,6 +9,7 @@
 #include "../../include/raman_mi355x.h"
 #include "common.hpp"
 #include "netspec.hpp"
+#include "host_util.hpp"
 
 namespace rdn {
 std::string pack(int arch, int dtype, const float* const* tensors, const int64_t* numels, int n, void* dst, size_t cap);
@@ -17,6 +19,9 @@ uint64_t get_corr_mask(const void* blob);
 uint64_t f16mix_default_mask(int arch);
 hipError_t launch_fused16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
 hipError_t launch_fused16_f16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
+hipError_t launch_fused16_f16_small(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
+                                   hipStream_t s);
+hipError_t launch_fused_inplace_short(const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
 hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                 hipStream_t s);
 
@@ -140,6 +145,18 @@ int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes)
   RDN_GUARD_END
 }
 
+// Latency geometry: a launch whose 640-row tiles would occupy at most half the CUs (the reference's
+// evaulate.py calls the model one spectrum at a time: 18 workgroups at L = 10,000) runs RDN_F16 /
+// RDN_F16MIX on 256-row tiles instead (2.8x the workgroups, each layer ~0.4x as long).  RDN_SHORT_TILES
+// = 0 / 1 forces either geometry (tests compare the two).
+static bool short_tiles(int arch, int64_t n, int64_t L, hipStream_t s) {
+  const char* env = std::getenv("RDN_SHORT_TILES");
+  if (env && (env[0] == '0' || env[0] == '1')) return env[0] == '1';
+  const int64_t T = rdn::H16_WB - 2 * rdn::fused_halo(arch), tiles = (L + T - 1) / T;
+  const int cus = rdn::device_cus(rdn::stream_device(s));
+  return cus > 0 && 2 * n * tiles <= cus;
+}
+
 int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* y, int64_t n, int64_t L, void* ws,
                 size_t ws_bytes, void* stream) {
   RDN_GUARD_BEGIN
@@ -160,9 +177,14 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
     return hip_check(rdn::launch_cbam_forward(arch, dtype, blob, x, y, n, (int)L, ws, ws_bytes, s), "cbam forward");
   }
   if (dtype == RDN_BF16) return hip_check(rdn::launch_fused16(arch, blob, x, y, n, (int)L, s), "fused bf16 forward");
-  if (dtype == RDN_F16) return hip_check(rdn::launch_fused16_f16(arch, blob, x, y, n, (int)L, s), "fused f16 forward");
+  const bool shrt = short_tiles(arch, n, L, s);
+  if (dtype == RDN_F16)
+    return hip_check(shrt ? rdn::launch_fused16_f16_small(arch, blob, x, y, n, (int)L, s)
+                          : rdn::launch_fused16_f16(arch, blob, x, y, n, (int)L, s), "fused f16 forward");
   if (dtype == RDN_F16MIX && arch != RDN_RRCDNET)
     return fail(RDN_EUNSUPPORTED, "RDN_F16MIX is built for RRCDNet; the other networks run RDN_F16");
+  if (dtype == RDN_F16MIX && shrt)
+    return hip_check(rdn::launch_fused_inplace_short(blob, x, y, n, (int)L, s), "fused f16mix forward (short tiles)");
   return hip_check(rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, s), "fused in-place forward");
   RDN_GUARD_END
 }

@@ -64,10 +64,14 @@
 namespace rdn {
 namespace H16_NS {
 
+#ifdef H16_TILE_ROWS
+constexpr int WB = H16_TILE_ROWS;                     // latency instantiation (fused16_small.hip): short tiles
+#else
 constexpr int WB = H16_WB;                            // 640 rows per tile, halo included
+#endif
 constexpr int ROWB = 128;                             // 64 channels x 16 bit
 constexpr uint32_t BUF_BYTES = WB * ROWB;             // 81920
-constexpr uint32_t LDS_BYTES = 2 * BUF_BYTES;         // 163840: the whole LDS of a CU
+constexpr uint32_t LDS_BYTES = 2 * BUF_BYTES;         // 163840 (640 rows): the whole LDS of a CU
 constexpr uint32_t BUF0 = 0, BUF1 = BUF_BYTES;
 constexpr int LAYER_BYTES = H16_LAYER_BYTES;          // [m 4][k-step 6][lane 64][8 x 16 bit] ... bias[64] f32
 constexpr int BIAS_OFF = H16_BIAS_OFF;
@@ -341,10 +345,14 @@ struct BAddr {
   }
 };
 
-#ifndef RDN_H16_LDSTEP
-#define RDN_H16_LDSTEP (RDN_H16_M32 ? 3 : 4)
+// steps between two of the next layer's operand loads: 4 on the 640-row tile (16x16x32: 3 is
+// -0.5 %, 2 is -2 %), as many as fit otherwise
+#ifdef RDN_H16_LDSTEP
+constexpr int LDSTEP = RDN_H16_LDSTEP;
+#else
+constexpr int LDSTEP = (KS * NT - 1) / (NLOAD - 1) < 4 ? (KS * NT - 1) / (NLOAD - 1) : 4;
 #endif
-static_assert(RDN_H16_LDSTEP * (NLOAD - 1) < KS * NT, "every operand load of the next layer must be issued");
+static_assert(LDSTEP >= 1 && LDSTEP * (NLOAD - 1) < KS * NT, "every operand load of the next layer must be issued");
 
 // One Conv1d(64, 64, 3, dilation=dil, padding=dil) over the tile, src -> dst: this wave's 32
 // output channels x NT N-tiles from the operands in F, while the next layer's operands stream into
@@ -438,9 +446,7 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
       if (n > 0 && s == 1) epilogue(n - 1, prev);
 #if !defined(RDN_ABLATE_NOALOAD)
       // the next layer's operands, one buffer load every LDSTEP-th step: the vector-memory traffic
-      // of the CU's 8 waves spreads over the layer (16x16x32: denser is slower, 2 steps -2 %,
-      // 3 steps -0.5 % against 4)
-      constexpr int LDSTEP = RDN_H16_LDSTEP;
+      // of the CU's 8 waves spreads over the layer
       if (has_next && k % LDSTEP == 0 && k / LDSTEP < NLOAD) load_op(tl, next, h, k / LDSTEP, lo, G);
 #endif
       __builtin_amdgcn_sched_barrier(0);

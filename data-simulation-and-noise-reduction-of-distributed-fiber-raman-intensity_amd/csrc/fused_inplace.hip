@@ -284,6 +284,18 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restr
   else rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles);
 }
 
+// RDN_F16MIX RRCDNet on 256-row tiles (the in-place body, both heads split): the latency geometry for
+// launches too small to fill the chip (launch_fused_inplace_short)
+template <int TAIL>
+__global__ __launch_bounds__(THREADS) void rrcdnet_short(const uint8_t* __restrict__ blob, const float* __restrict__ x,
+                                                         float* __restrict__ y, int L, int T, int tiles) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int n;
+  Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
+  if (tl.base >= 0 && tl.base + TileGeo<2>::WB <= L) rrcdnet_body<MODE_H8, false, 2, TAIL>(tl, y, n, L, T);
+  else rrcdnet_body<MODE_H8, true, 2, TAIL>(tl, y, n, L, T);
+}
+
 #define IP_KERNEL(name, arch)                                                                              \
   template <int MODE, int TAIL = 0>                                                                         \
   __global__ __launch_bounds__(THREADS) void name(const uint8_t* __restrict__ blob, const float* __restrict__ x, \
@@ -327,6 +339,22 @@ static fused_kernel_t pick(int arch) {
     case PIDN: return ip::pidn<MODE>;
     default: return nullptr;
   }
+}
+
+// RDN_F16MIX RRCDNet with 256-row tiles (ip::rrcdnet_short)
+hipError_t launch_fused_inplace_short(const uint8_t* blob, const float* x, float* y, int64_t n, int L,
+                                      hipStream_t stream) {
+  const fused_kernel_t k = ip::rrcdnet_short<ip::RRCDNET_F16MIX_TAIL>;
+  const hipError_t e = ensure_dynamic_lds((const void*)k, 92, (int)ip::TileGeo<2>::LDS, stream_device(stream));
+  if (e != hipSuccess) return e;
+  const int H = fused_halo(RRCDNET), T = ip::TileGeo<2>::WB - 2 * H, tiles = (L + T - 1) / T;
+  const int64_t chunk = (int64_t)(0x7fffffff / tiles);
+  for (int64_t n0 = 0; n0 < n; n0 += chunk) {
+    const int64_t nn = n - n0 < chunk ? n - n0 : chunk;
+    hipLaunchKernelGGL(k, dim3((unsigned)(nn * tiles)), dim3(THREADS), ip::TileGeo<2>::LDS, stream, blob, x + n0 * L,
+                       y + n0 * L, L, T, tiles);
+  }
+  return hipGetLastError();
 }
 
 // dtype: F32 (exact fp32), BF16X3 (split bf16) or F16F8 (f16 + e4m3 correction); see common.hpp

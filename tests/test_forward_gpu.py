@@ -76,13 +76,24 @@ def test_fp32_matches_reference(arch, which, inputs):
         assert ok, f"{arch}/{which}/{name}: fp32 {msg}"
 
 
-@pytest.mark.parametrize("dtype", ["f16", "f16f8", "bf16x3"])
+def _tiles(dtype, monkeypatch):
+    """'f16' runs on the 640-row tiles, 'f16-short' on the 256-row latency tiles (abi.cpp short_tiles,
+    RDN_SHORT_TILES forces the geometry): returns the module dtype."""
+    if dtype in ("f16", "f16-short"):
+        monkeypatch.setenv("RDN_SHORT_TILES", "1" if dtype == "f16-short" else "0")
+        return "f16"
+    return dtype
+
+
+@pytest.mark.parametrize("dtype", ["f16", "f16-short", "f16f8", "bf16x3"])
 @pytest.mark.parametrize("arch,which", _cases(FUSED))
-def test_16bit_within_tolerance(arch, which, dtype, inputs):
+def test_16bit_within_tolerance(arch, which, dtype, inputs, monkeypatch):
     """The 16-bit modes against the reference fp32 forward: max-abs <= 2e-2 (trained weights,
     normalised-intensity outputs), 2e-2 * max(1, max|ref|) for the synthetic weight sets."""
+    if dtype == "f16-short" and arch in ("ADSDN", "APIDN"):
+        pytest.skip("the CBAM networks run the team kernel at every batch size")
     g = load_golden(arch)
-    m = _model(arch, which, dtype)
+    m = _model(arch, which, _tiles(dtype, monkeypatch))
     for name in INPUT_SETS:
         ref = g[f"{which}_{name}"]
         y = _run(m, input_array(inputs, name))
@@ -93,14 +104,17 @@ def test_16bit_within_tolerance(arch, which, dtype, inputs):
         assert err <= tol, f"{arch}/{which}/{name}: {dtype} max-abs error {err:.3e} > {tol:.1e}"
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "f16", "bf16x3", "f16f8"])
+@pytest.mark.parametrize("dtype", ["fp32", "f16", "f16-short", "bf16x3", "f16f8"])
 @pytest.mark.parametrize("arch", FUSED)
-@pytest.mark.parametrize("L", [1, 2, 5, 453, 454, 455, 908, 2049])
-def test_ragged_lengths_vs_oracle(arch, L, dtype):
-    """Tile-boundary and tiny-L cases (T = 512 - 2*halo) against the CPU oracle."""
+@pytest.mark.parametrize("L", [1, 2, 5, 197, 198, 199, 453, 454, 455, 908, 2049])
+def test_ragged_lengths_vs_oracle(arch, L, dtype, monkeypatch):
+    """Tile-boundary and tiny-L cases (T = 512 - 2*halo, 640 - 2*halo, 256 - 2*halo) against the CPU
+    oracle."""
     from oracle.models import forward as oracle_forward
+    if dtype == "f16-short" and arch in ("ADSDN", "APIDN"):
+        pytest.skip("the CBAM networks run the team kernel at every batch size")
     sd = golden_state_dict(arch, "synth")
-    m = _model(arch, "synth", dtype)
+    m = _model(arch, "synth", _tiles(dtype, monkeypatch))
     rng = np.random.default_rng(L)
     x = rng.uniform(-0.2, 1.2, (3, L)).astype(np.float32)
     y = _run(m, x)
@@ -109,6 +123,19 @@ def test_ragged_lengths_vs_oracle(arch, L, dtype):
     err = np.abs(y - ref).max()
     tol = F32_REL * scale if dtype == "fp32" else BF16_ABS * max(1.0, scale)
     assert err <= tol, f"{arch} L={L} {dtype}: {err:.3e} > {tol:.3e}"
+
+
+@pytest.mark.parametrize("arch", ["DenoiseCNN", "DSDN", "PIDN"])
+def test_short_tiles_bitwise_equal(arch, monkeypatch):
+    """RDN_F16 on the 256-row latency tiles and on the 640-row tiles computes every output position
+    from the same operands in the same MFMA K order: bitwise identical outputs."""
+    m = _model(arch, "trained", "f16")
+    x = np.random.default_rng(7).uniform(0, 1, (2, 3001)).astype(np.float32)
+    monkeypatch.setenv("RDN_SHORT_TILES", "0")
+    y_long = _run(m, x)
+    monkeypatch.setenv("RDN_SHORT_TILES", "1")
+    y_short = _run(m, x)
+    assert np.array_equal(y_long, y_short)
 
 
 def test_batch_independence_and_determinism():
