@@ -64,10 +64,13 @@ typedef enum {
  *              value.
  *   RDN_F16MIX RRCDNet only: RDN_F16 arithmetic with the RDN_F16F8 correction kept on the last three
  *              layers of the right branch (the ones the head's cancellation x - (r + l)/2 amplifies):
- *              within 2e-2 (1.4e-2 on trained RRCDNet).  One hybrid kernel: the plain layers on the
- *              RDN_F16 ping-pong engine, the corrected ones and the heads on the in-place tile.  The
- *              corrected layers are compiled in; rdn_get_correction_mask reads them back from a
- *              packed blob. */
+ *              within 2e-2 (1.4e-2 on trained RRCDNet).  One hybrid kernel: the plain layers, the
+ *              whole left branch and its head on the RDN_F16 ping-pong engine, the right branch's
+ *              last four layers and head on the in-place tile.  The corrected layers are compiled in;
+ *              rdn_get_correction_mask reads them back from a packed blob.
+ * RDN_F16 / RDN_F16MIX launches that would occupy at most half the CUs with 640-row tiles (e.g. one
+ * spectrum per call, evaulate.py:29-32) run on 256-row tiles (same arithmetic; RDN_F16MIX then runs
+ * every layer on the in-place tile); the environment variable RDN_SHORT_TILES=0/1 forces either. */
 typedef enum { RDN_F32 = 0, RDN_BF16 = 1, RDN_BF16X3 = 2, RDN_F16F8 = 3, RDN_F16 = 4, RDN_F16MIX = 5 } rdn_dtype;
 
 enum {
