@@ -908,24 +908,31 @@ __device__ __forceinline__ float quarter_max(float v) {
 // per-channel sum / max of u (BUF0) over the tile's own positions and its edge rows -> slot (sc1);
 // arrive at the team counter
 __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& ta, char* slot, unsigned* ctr,
-                                          bool arrive) {
+                                          bool arrive, const h16c::ChanStats* pre) {
   char* lds = tl.lds;
   const Lane ln;
   const int tid = h16c::tid();
   const int H = ta.halo, T = ta.T;
   const int rend = H + min(T, tl.L - tl.base - H);
+  // this lane's channel partials: accumulated by the conv that produced u (pre: its epilogue, from
+  // the unrounded values), or from u in BUF0
   h16c::f32x8 sm = (h16c::f32x8)(0.f), mx = (h16c::f32x8)(-INFINITY);
-  const char* b0 = lds + h16c::BUF0 + (ln.h ? tl.koff[2][1] : tl.koff[2][0]);
-  V uv[NT];
+  if (pre) {
+    sm = pre->sum;
+    mx = pre->max;
+  } else {
+    const char* b0 = lds + h16c::BUF0 + (ln.h ? tl.koff[2][1] : tl.koff[2][0]);
+    V uv[NT];
 #pragma unroll
-  for (int n = 0; n < NT; ++n) uv[n] = *(const V*)(b0 + n * 16 * h16c::ROWB);
+    for (int n = 0; n < NT; ++n) uv[n] = *(const V*)(b0 + n * 16 * h16c::ROWB);
 #pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    const int r = ln.row(n);
-    if (r >= H && r < rend) {
-      const h16c::f32x8 u = __builtin_convertvector(uv[n], h16c::f32x8);
-      sm += u;
-      mx = __builtin_elementwise_max(mx, u);
+    for (int n = 0; n < NT; ++n) {
+      const int r = ln.row(n);
+      if (r >= H && r < rend) {
+        const h16c::f32x8 u = __builtin_convertvector(uv[n], h16c::f32x8);
+        sm += u;
+        mx = __builtin_elementwise_max(mx, u);
+      }
     }
   }
 #pragma unroll
@@ -1156,11 +1163,19 @@ __device__ __forceinline__ void team16_spectra(char* lds, const uint8_t* blob, c
     h16c::Tile tl = h16c::init_tile(lds, blob, big16, x + (size_t)n * L, L, tile * ta.T - ta.halo);
     h16c::Frags F0, F1;
     V id[NT];
-    auto cbam = [&](int slot, int res) {
+    h16c::ChanStats cs;
+    auto conv2_stats = [&]() -> h16c::ChanStats* {   // the block's conv2 accumulates u's statistics
+      cs.sum = (h16c::f32x8)(0.f);
+      cs.max = (h16c::f32x8)(-INFINITY);
+      cs.lo = ta.halo;
+      cs.hi = ta.halo + min(ta.T, L - tl.base - ta.halo);
+      return &cs;
+    };
+    auto cbam = [&](int slot, int res, const h16c::ChanStats* pre) {
       char* mine = tslots + ((size_t)(nbar & 1) * ta.TT + tile) * SLOT16_BYTES;
       const bool skip = ta.force_miss > 0 && __builtin_amdgcn_workgroup_id_x() == 0 && nbar + 1 == (unsigned)ta.force_miss;
       st(1);
-      publish16(tl, ta, mine, ctr, !skip);
+      publish16(tl, ta, mine, ctr, !skip, pre);
       st(3);
       team_wait(ta, ctr, (nbar + 1) * (unsigned)ta.TT);
       st(4);
@@ -1174,22 +1189,22 @@ __device__ __forceinline__ void team16_spectra(char* lds, const uint8_t* blob, c
     if (ADS) {
       // ADSDN/train.py:160-167: cbam(relu(conv_ds x)); relu(conv1); relu(conv2); cbam;
       // 15 x relu(cbam(bn2(conv2(relu(bn1(conv1 x))))) + x); conv_out
-      cbam(2, RES_NONE);
+      cbam(2, RES_NONE, nullptr);
       h16c::layer<h16c::RELU, EDGE>(tl, h16c::BUF0, h16c::BUF1, 1, F0, F1);
       h16c::layer<h16c::RELU, EDGE>(tl, h16c::BUF1, h16c::BUF0, 1, F1, F0);
-      cbam(5, RES_NONE);
+      cbam(5, RES_NONE, nullptr);
       for (int b = 0; b < 15; ++b) {
         h16c::layer<h16c::RELU, EDGE>(tl, h16c::BUF0, h16c::BUF1, 1, F0, F1);
-        h16c::layer<h16c::LINEAR_SAVE, EDGE>(tl, h16c::BUF1, h16c::BUF0, 1, F1, F0, true, id);
-        cbam(8 + 3 * b, RES_ADD_RELU);
+        h16c::layer<h16c::LINEAR_SAVE, EDGE>(tl, h16c::BUF1, h16c::BUF0, 1, F1, F0, true, id, conv2_stats());
+        cbam(8 + 3 * b, RES_ADD_RELU, &cs);
       }
     } else {
       // APIDN/train.py:150-159: h = relu(conv_ds x); 15 x x += cbam(bn(conv(relu(bn(conv x)))));
       // sigmoid(conv_out(x + h))
       for (int b = 0; b < 15; ++b) {
         h16c::layer<h16c::RELU, EDGE>(tl, h16c::BUF0, h16c::BUF1, 1, F0, F1);
-        h16c::layer<h16c::LINEAR_SAVE, EDGE>(tl, h16c::BUF1, h16c::BUF0, 1, F1, F0, true, id);
-        cbam(2 + 3 * b, RES_ADD);
+        h16c::layer<h16c::LINEAR_SAVE, EDGE>(tl, h16c::BUF1, h16c::BUF0, 1, F1, F0, true, id, conv2_stats());
+        cbam(2 + 3 * b, RES_ADD, &cs);
       }
       h16c::stem<true>(tl, 0, h16c::BUF0);       // + h, recomputed from x
       h16c::lds_barrier();

@@ -357,9 +357,17 @@ static_assert(LDSTEP >= 1 && LDSTEP * (NLOAD - 1) < KS * NT, "every operand load
 // One Conv1d(64, 64, 3, dilation=dil, padding=dil) over the tile, src -> dst: this wave's 32
 // output channels x NT N-tiles from the operands in F, while the next layer's operands stream into
 // G (header).
+// Per-channel sum / max of a layer's output over tile rows [lo, hi), accumulated in its epilogue
+// from the unrounded fp32 values: this lane's 8 channels (slot 4h + q) over its rows (the CBAM
+// channel statistics of the conv that produces u, cbam.hip team16_forward)
+struct ChanStats {
+  f32x8 sum, max;
+  int lo, hi;
+};
+
 template <int EPI, bool EDGE>
 __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int dil, const Frags& F, Frags& G,
-                                      bool has_next = true, V* idv = nullptr) {
+                                      bool has_next = true, V* idv = nullptr, ChanStats* cs = nullptr) {
   static_assert(EPI != LINEAR_SAVE || !RDN_H16_M32, "LINEAR_SAVE: one slot per N-tile");
   const int lane = tid() & 63, w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB;
   const int next = tl.layer + 1;
@@ -421,7 +429,17 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     const bool valid = !EDGE || in_range(pos0 + NR * n + (lane & 15), tl.L);
     V* p = (V*)(tl.lds + sa + n * NR * ROWB);
     if constexpr (EPI == LINEAR_SAVE) idv[n] = *p;
-    store_slot(p, __builtin_shufflevector(a.v[0], a.v[1], 0, 1, 2, 3, 4, 5, 6, 7), valid);
+    const f32x8 v = __builtin_shufflevector(a.v[0], a.v[1], 0, 1, 2, 3, 4, 5, 6, 7);
+    if constexpr (EPI == LINEAR_SAVE) {
+      if (cs) {
+        const int r = pos0 - tl.base + NR * n + (lane & 15);
+        if (r >= cs->lo && r < cs->hi) {
+          cs->sum += v;
+          cs->max = __builtin_elementwise_max(cs->max, v);
+        }
+      }
+    }
+    store_slot(p, v, valid);
   };
 #endif
 
