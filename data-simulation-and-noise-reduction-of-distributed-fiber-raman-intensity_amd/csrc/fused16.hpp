@@ -523,7 +523,13 @@ __device__ __forceinline__ void head(Tile& tl, uint32_t src, const Frags& F, Fra
         acc.v[0] = mma(F.a[s], B[k % (PF + 1)], s == 0 ? F.bias[0] : acc.v[0]);
 #endif
       }
-      if (has_next && k % 2 == 0 && k / 2 < NLOAD) load_op(tl, next, h, k / 2, lo, G);
+      // the next layer's NLOAD operand loads spread over the head's K steps (operand i at step
+      // i * K / NLOAD: every one is issued however few N-tiles the head has)
+      if (has_next) {
+#pragma unroll
+        for (int i = 0; i < NLOAD; ++i)
+          if (i * K / NLOAD == k) load_op(tl, next, h, i, lo, G);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
 #if RDN_H16_M32

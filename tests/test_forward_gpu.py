@@ -125,11 +125,12 @@ def test_ragged_lengths_vs_oracle(arch, L, dtype, monkeypatch):
     assert err <= tol, f"{arch} L={L} {dtype}: {err:.3e} > {tol:.3e}"
 
 
-@pytest.mark.parametrize("arch", ["DenoiseCNN", "DSDN", "PIDN"])
+@pytest.mark.parametrize("arch", ["DenoiseCNN", "RRCDNet", "DSDN", "PIDN"])
 def test_short_tiles_bitwise_equal(arch, monkeypatch):
     """RDN_F16 on the 256-row latency tiles and on the 640-row tiles computes every output position
-    from the same operands in the same MFMA K order: bitwise identical outputs."""
-    m = _model(arch, "trained", "f16")
+    from the same operands in the same MFMA K order: bitwise identical outputs (RRCDNet: plain RDN_F16,
+    whose right head prefetches the left branch's first layer within its 2 N-tiles)."""
+    m = _model(arch, "trained", "f16-plain" if arch == "RRCDNet" else "f16")
     x = np.random.default_rng(7).uniform(0, 1, (2, 3001)).astype(np.float32)
     monkeypatch.setenv("RDN_SHORT_TILES", "0")
     y_long = _run(m, x)
