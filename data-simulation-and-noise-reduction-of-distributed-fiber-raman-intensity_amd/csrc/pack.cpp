@@ -558,7 +558,7 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
 // meets the 2e-2 bar on every golden fixture except trained RRCDNet (3.5e-2 fused / 2.6e-2 with the
 // exact head input of the in-place path); the head's cancellation x - (r + l)/2 amplifies the
 // rounding of the right branch's last layers most (tools/f16mix_select.py, greedy on the GPU), and
-// correcting right_net.15-17 (big layers 12-14) brings it to 1.36e-2 (tools/f16mix_masks.py).  The
+// correcting right_net.15-17 (big layers 12-14) brings it to 1.36e-2 with both heads split, 1.65e-2 with the left head in plain f16 (tools/f16mix_masks.py).  The
 // pattern is compiled into the kernel (fused_inplace.hip RRCDNET_F16MIX_TAIL); the blob records it.
 uint64_t f16mix_default_mask(int arch) {
   return arch == RRCDNET ? (0x7ull << 12) : 0;

@@ -64,7 +64,7 @@ typedef enum {
  *              value.
  *   RDN_F16MIX RRCDNet only: RDN_F16 arithmetic with the RDN_F16F8 correction kept on the last three
  *              layers of the right branch (the ones the head's cancellation x - (r + l)/2 amplifies):
- *              within 2e-2 (1.4e-2 on trained RRCDNet).  One hybrid kernel: the plain layers, the
+ *              within 2e-2 (1.65e-2 on trained RRCDNet).  One hybrid kernel: the plain layers, the
  *              whole left branch and its head on the RDN_F16 ping-pong engine, the right branch's
  *              last four layers and head on the in-place tile.  The corrected layers are compiled in;
  *              rdn_get_correction_mask reads them back from a packed blob.
