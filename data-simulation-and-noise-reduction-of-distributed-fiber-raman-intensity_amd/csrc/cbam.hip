@@ -859,9 +859,7 @@ constexpr int RED16_OFF = SC;                                  // [4 row blocks]
 constexpr int SLP_OFF = RED16_OFF + 2 * 4 * 64 * 4;            // [8 waves][64] f64 slot partials, then u32
 constexpr int POOL_OFF = SLP_OFF + 8 * 64 * 12;                // [2][64] f64: pooled avg / max
 constexpr int CA16_OFF = POOL_OFF + 2 * 64 * 8;                // channel attention, one copy per wave (8 x 64 f32)
-constexpr int S1H_OFF = CA16_OFF + 8 * 64 * 4;                 // [2 halves][WB16] partial sums over 32 channels
-constexpr int S2H_OFF = S1H_OFF + 2 * WB16 * 4;                // [2 halves][WB16] partial maxima
-constexpr int SA16_OFF = S2H_OFF + 2 * WB16 * 4;               // spatial attention per tile row
+constexpr int SA16_OFF = CA16_OFF + 8 * 64 * 4;                // spatial attention per tile row
 constexpr int M1_OFF = SA16_OFF + WB16 * 4;                    // [mean_c; max_c] map, rows -3 .. WB + 2
 constexpr int M2_OFF = M1_OFF + (WB16 + 8) * 4;
 static_assert(M2_OFF + (WB16 + 8) * 4 <= (int)h16c::LDS_BYTES, "CBAM scratch fits BUF1");
@@ -1075,60 +1073,71 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   caw[lane] = cav;
   st(11);
 
-  // spatial statistics of u*ca: per item 8 channels in packed f16 (the mode's storage precision:
-  // u is f16, ca rounds to f16), the partial sum / max to f32, the 4 quarters of a wave (32
-  // channels) by lane swaps, the two channel halves through LDS
+  // spatial statistics of u*ca in packed f16 (the mode's storage precision: u is f16, ca rounds to
+  // f16): wave w takes rows 80w .. 80w + 79, lane (q, c16) the rows 80w + c16 + 16k (k < 5) at
+  // slots q and q + 4 (16 channels), the 4 quarters (all 64 channels) by lane swaps -- every row's
+  // [mean; max] completes inside one wave; partial sums / maxima to f32
   char* b0 = lds + h16c::BUF0 + (ln.h ? tl.koff[2][1] : tl.koff[2][0]);
   typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-  V cah;
+  V cah, cq0, cq4;           // ca of this lane's pointwise slot; of slots q and q + 4
 #pragma unroll
-  for (int j = 0; j < 8; ++j) cah[j] = (_Float16)caw[h16_channel(ln.slot(), j)];
-  float* s1h = (float*)(lds + S1H_OFF);
-  float* s2h = (float*)(lds + S2H_OFF);
-  V uv[NT];                  // all reads first: one LDS round trip for the pass, not one per item
+  for (int j = 0; j < 8; ++j) {
+    cah[j] = (_Float16)caw[h16_channel(ln.slot(), j)];
+    cq0[j] = (_Float16)caw[h16_channel(ln.q, j)];
+    cq4[j] = (_Float16)caw[h16_channel(ln.q + 4, j)];
+  }
+  float* m1 = (float*)(lds + M1_OFF) + 3;      // [mean_c; max_c] of rows -3 .. WB + 2, zero outside
+  float* m2 = (float*)(lds + M2_OFF) + 3;      // the tile and [0, L)
+  constexpr int SROWS = WB16 / h16c::WAVES;    // 80 rows per wave
+  static_assert(SROWS % 16 == 0, "whole 16-row groups per wave");
+  {
+    V ua[SROWS / 16], ub[SROWS / 16];
 #pragma unroll
-  for (int n = 0; n < NT; ++n) uv[n] = *(const V*)(b0 + n * 16 * h16c::ROWB);
+    for (int k = 0; k < SROWS / 16; ++k) {
+      const int r = SROWS * w + ln.c16 + 16 * k;
+      ua[k] = *(const V*)(lds + h16c::BUF0 + h16c::soff(r, ln.q));
+      ub[k] = *(const V*)(lds + h16c::BUF0 + h16c::soff(r, ln.q + 4));
+    }
 #pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    const V v = uv[n] * cah;
-    const h2 s01 = __builtin_shufflevector(v, v, 0, 1) + __builtin_shufflevector(v, v, 2, 3);
-    const h2 s45 = __builtin_shufflevector(v, v, 4, 5) + __builtin_shufflevector(v, v, 6, 7);
-    const h2 m01 = __builtin_elementwise_max(__builtin_shufflevector(v, v, 0, 1), __builtin_shufflevector(v, v, 2, 3));
-    const h2 m45 = __builtin_elementwise_max(__builtin_shufflevector(v, v, 4, 5), __builtin_shufflevector(v, v, 6, 7));
-    const h2 ss = s01 + s45, mm = __builtin_elementwise_max(m01, m45);
-    float sm = (float)ss[0] + (float)ss[1];
-    float mx = fmaxf((float)mm[0], (float)mm[1]);
-    sm = quarter_sum(sm);
-    mx = quarter_max(mx);
-    if (ln.q == 0) {
-      s1h[ln.h * WB16 + ln.row(n)] = sm;
-      s2h[ln.h * WB16 + ln.row(n)] = mx;
+    for (int k = 0; k < SROWS / 16; ++k) {
+      const V va = ua[k] * cq0, vb = ub[k] * cq4;
+      const V vs = va + vb, vm = __builtin_elementwise_max(va, vb);
+      const h2 s2 = (__builtin_shufflevector(vs, vs, 0, 1) + __builtin_shufflevector(vs, vs, 2, 3)) +
+                    (__builtin_shufflevector(vs, vs, 4, 5) + __builtin_shufflevector(vs, vs, 6, 7));
+      const h2 x2 = __builtin_elementwise_max(
+          __builtin_elementwise_max(__builtin_shufflevector(vm, vm, 0, 1), __builtin_shufflevector(vm, vm, 2, 3)),
+          __builtin_elementwise_max(__builtin_shufflevector(vm, vm, 4, 5), __builtin_shufflevector(vm, vm, 6, 7)));
+      const float sm = quarter_sum((float)s2[0] + (float)s2[1]);
+      const float mx = quarter_max(fmaxf((float)x2[0], (float)x2[1]));
+      if (ln.q == 0) {
+        const int r = SROWS * w + ln.c16 + 16 * k;
+        const bool in = h16c::in_range(tl.base + r, tl.L);
+        m1[r] = in ? sm * (1.0f / 64.0f) : 0.f;
+        m2[r] = in ? mx : 0.f;
+      }
+    }
+    if (tid < 6) {                             // rows beyond the tile feed only halo rows: 0
+      const int r = tid < 3 ? tid - 3 : WB16 + tid - 3;
+      m1[r] = 0.f;
+      m2[r] = 0.f;
     }
   }
   __syncthreads();
   st(12);
-  // the [mean; max] map over window rows -3 .. WB + 2 (index r + 3), zero outside the tile and [0, L)
-  float* m1 = (float*)(lds + M1_OFF);
-  float* m2 = (float*)(lds + M2_OFF);
-  for (int i = tid; i < WB16 + 6; i += h16c::THREADS) {
-    const int rr = i - 3, p = tl.base + rr;
-    const bool in = rr >= 0 && rr < WB16 && p >= 0 && p < tl.L;
-    m1[i] = in ? (s1h[rr] + s1h[WB16 + rr]) * (1.0f / 64.0f) : 0.f;
-    m2[i] = in ? fmaxf(s2h[rr], s2h[WB16 + rr]) : 0.f;
-  }
-  __syncthreads();
+  // sa = sigmoid(conv7([mean_c; max_c]))
   float* sa = (float*)(lds + SA16_OFF);
   for (int r = tid; r < WB16; r += h16c::THREADS) {
     float a = bias ? cmisc[82] : 0.f;
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-      a = fmaf(cmisc[68 + k], m1[r + k], a);
-      a = fmaf(cmisc[75 + k], m2[r + k], a);
+      a = fmaf(cmisc[68 + k], m1[r + k - 3], a);
+      a = fmaf(cmisc[75 + k], m2[r + k - 3], a);
     }
     sa[r] = sigm(a);
   }
   __syncthreads();
   st(13);
+  V uv[NT];
   // h = [identity +] u*ca*sa [relu], in place, packed f16; rows outside [0, L) zero
   float sv[NT];
 #pragma unroll
