@@ -11,11 +11,29 @@ fused gfx950 kernels of ``csrc/``.
 Supported: eval mode, CUDA float32 input ``(N, 1, L)``.  Training mode, CPU tensors and
 ``requires_grad`` inputs raise (the engine is inference-only).
 """
+import operator
+
 import torch
 import torch.nn as nn
 from torch.nn import init
 
 from . import engine
+
+# Registration generation: bumped whenever any module anywhere registers (or re-assigns) a parameter,
+# buffer or submodule (torch's global registration hooks), so the pack-cache below re-derives its
+# tensor list only then instead of re-checking 156 dict slots on every forward.
+_REG_GEN = [0]
+
+
+def _on_registration(*_):
+    _REG_GEN[0] += 1          # returns None: the registered object is kept as is
+
+
+for _reg in ("register_module_parameter_registration_hook", "register_module_buffer_registration_hook",
+             "register_module_module_registration_hook"):
+    getattr(nn.modules.module, _reg)(_on_registration)
+_VERSION = operator.attrgetter("_version")
+_DATA_PTR = torch.Tensor.data_ptr
 
 C = 64
 
@@ -40,6 +58,7 @@ class _EngineNet(nn.Module):
         self._packed = None
         self._packed_key = None
         self._tensor_cache = None
+        self._cache_gen = -1
 
     # -- configuration -----------------------------------------------------------------------
     @property
@@ -70,25 +89,29 @@ class _EngineNet(nn.Module):
 
     # -- packing -----------------------------------------------------------------------------
     def _slots(self):
-        """(owner dict, name, tensor) of every parameter and buffer, cached: the pack key below is
-        rebuilt on every forward (the reference evaluate loop is batch-1, evaulate.py:29-32), and
-        rebuilding state_dict() there costs more than a small forward.  The cache is re-derived
-        whenever any slot no longer holds the tensor it recorded (a parameter or buffer replaced
-        anywhere in the tree, .to() / _apply swapping storages)."""
-        c = self._tensor_cache
-        if c is None or any(d.get(k) is not t for d, k, t in c):
+        """Every parameter and buffer tensor of the tree, cached: the pack key below is rebuilt on
+        every forward (the reference evaluate loop is batch-1, evaulate.py:29-32), and rebuilding
+        state_dict() there costs more than a small forward.  Re-derived when any parameter, buffer or
+        submodule was (re)registered anywhere since (_REG_GEN) and after _apply (.to(), .cuda())."""
+        if self._tensor_cache is None or self._cache_gen != _REG_GEN[0]:
             c = []
             for mod in self.modules():
                 for d in (mod._parameters, mod._buffers):
-                    c.extend((d, k, t) for k, t in d.items() if t is not None)
+                    c.extend(t for t in d.values() if t is not None)
             self._tensor_cache = c
-        return c
+            self._cache_gen = _REG_GEN[0]
+        return self._tensor_cache
+
+    def _apply(self, fn, *args, **kwargs):
+        self._tensor_cache = None                 # storages swapped (param.data = fn(param.data))
+        return super()._apply(fn, *args, **kwargs)
 
     def _state_key(self, device):
-        # identity + storage + version counter of each tensor: in-place updates (optimizer steps,
-        # .add_(), load_state_dict's copy_) bump _version; replacements change identity or storage
-        return (str(device), self._engine_code,
-                tuple((t.data_ptr(), t._version) for _, _, t in self._slots()), len(self._tensor_cache))
+        # in-place updates (optimizer steps, .add_(), load_state_dict's copy_) bump _version, and the
+        # version counters only grow, so their sum changes with any of them; storage swaps
+        # (.data = ...) change a data_ptr; replaced tensors re-derive the list (_slots)
+        ts = self._slots()
+        return (str(device), self._engine_code, id(ts), sum(map(_VERSION, ts)), tuple(map(_DATA_PTR, ts)))
 
     def packed_weights(self, device):
         key = self._state_key(device)
