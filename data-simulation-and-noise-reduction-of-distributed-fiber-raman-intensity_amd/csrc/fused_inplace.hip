@@ -12,6 +12,12 @@
 #define H16_LAYER_BYTES BIG_BYTES_H8
 #define H16_BIAS_OFF H8_BIAS_OFF
 #include "fused16.hpp"
+// the same over 256-row tiles: the ping-pong part of RDN_F16MIX's latency geometry (rrcdnet_short)
+#undef H16_NS
+#define H16_NS h16xs
+#define H16_TILE_ROWS 256
+#include "fused16.hpp"
+#undef H16_TILE_ROWS
 
 namespace rdn {
 namespace ip {
@@ -184,90 +190,20 @@ constexpr int RRCDNET_F16MIX_TAIL = 3;
 // fragments of the H8 blob start with fused16's [m][k-step][lane][8 x f16] map (pack.cpp
 // pack_big_h8 / pack_big_bf16, same h16_channel K order), so both halves read one blob.
 
-// ping-pong buffer `src` (640 rows x 128 B, fused16 slot swizzle) -> the f16 plane of the in-place
-// tile (640 rows x 256 B, off_f32 swizzle).  The two overlap: everything is read before anything
-// is written.
-__device__ __forceinline__ void pingpong_to_tile(char* lds, uint32_t src) {
-  constexpr int ITEMS = h16x::WB * 8 / THREADS;          // 10 (row, slot) items per thread
-  static_assert(h16x::WB * 8 % THREADS == 0 && h16x::WB == TileGeo<5>::WB, "one 640-row tile");
-  const int t = opaque_tid();
-  f16x8 v[ITEMS];
-#pragma unroll
-  for (int i = 0; i < ITEMS; ++i) {
-    const int item = t + THREADS * i, row = item >> 3, slot = item & 7;
-    v[i] = *(const f16x8*)(lds + src + h16x::soff(row, slot));
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < ITEMS; ++i) {
-    const int item = t + THREADS * i, row = item >> 3, slot = item & 7;
-    *(f16x8*)(lds + off_f32(row, 16 * slot)) = v[i];
-  }
-  __syncthreads();
-}
-
-template <bool EDGE, int TAIL>
-__device__ __forceinline__ void rrcdnet_hybrid_body(Tile& tl, const uint8_t* blob, const float* x, float* y, int n,
-                                                    int L, int T, int tiles) {
-  constexpr int H = fused_halo(RRCDNET), NBK = 5, PP = 14 - TAIL;   // ping-pong layers of the right branch
-  using HO = HeadOut<MODE_H8, NBK>;
-  int n16;
-  h16x::Tile t16 = h16x::make_tile(tl.lds, blob, x, L, T, tiles, H, n16);
-  static_assert(PP % 2 == 1, "the ping-pong run ends on F0 -> BUF1");
-  h16x::Frags F0, F1;            // alternating operand buffers (fused16.hpp layer)
-  h16x::load_frags(t16, 0, F0);
-  h16x::stem(t16, 0, h16x::BUF0);
-  h16x::lds_barrier();
-  for (int i = 0; i < PP / 2; ++i) {
-    h16x::layer<h16x::RELU, EDGE>(t16, h16x::BUF0, h16x::BUF1, 1, F0, F1);
-    h16x::layer<h16x::RELU, EDGE>(t16, h16x::BUF1, h16x::BUF0, 1, F1, F0);
-  }
-  h16x::layer<h16x::RELU, EDGE>(t16, h16x::BUF0, h16x::BUF1, 1, F0, F1, false);
-  uint32_t cur = h16x::BUF1;
-  f32x4 id[16 * NBK / 4];
-  LayerA<MODE_H8> a;
-  tl.layer = PP;
-  load_layer_a<MODE_H8>(tl, PP, a);
-  pingpong_to_tile(tl.lds, cur);
-  conv<MODE_H8, RELU, 1, EDGE, NBK, false, true, true>(tl, 1, id, a, true);       // writes the e4m3 planes
-  for (int i = 0; i < TAIL; ++i) conv<MODE_H8, RELU, 1, EDGE, NBK, true, true, true>(tl, 1, id, a, i + 1 < TAIL);
-  double r[HO::ROWS];
-  head<MODE_H8, NBK>(tl, 2, r);
-  park_rows<MODE_H8, NBK>(tl, y, n, r, H, T);
-  // left branch: layers 15-28 and the head on the ping-pong engine (f16 activations into the head,
-  // whose weights carry their rounding residue: tools/head_fusion_emul.py puts this at 1.52e-2 on
-  // trained RRCDNet against 1.44e-2 with the split head, the bar being 2e-2)
-  t16.layer = 15;
-  h16x::load_frags(t16, 15, F0);
-  __syncthreads();               // the left stem overwrites the rows the right head just read
-  h16x::stem(t16, 1, h16x::BUF0);
-  h16x::lds_barrier();
-  for (int i = 0; i < 7; ++i) {  // left layers 15-28 (the one at 22 with d = 1)
-    h16x::layer<h16x::RELU, EDGE>(t16, h16x::BUF0, h16x::BUF1, 2, F0, F1);
-    h16x::layer<h16x::RELU, EDGE>(t16, h16x::BUF1, h16x::BUF0, 2 * i + 1 == 7 ? 1 : 2, F1, F0);
-  }
-  float l[h16x::HN];
-  h16x::head<EDGE>(t16, h16x::BUF0, F0, F1, false, l);
-  // hand the left head's rows (ping-pong lane layout) to the right head's (HeadOut) through LDS
-  // (BUF1: no longer read), then y = x - (r + l)/2 with r from its parking place in y
-  float* lrow = (float*)(tl.lds + h16x::BUF1);
-  if ((h16x::tid() & 63) < h16x::HEAD_LANES) {
-#pragma unroll
-    for (int k = 0; k < h16x::HN; ++k) {
-      const int j = h16x::head_row(k);
-      if (j < h16x::WB) lrow[j] = l[k];
-    }
-  }
-  h16x::lds_barrier();
-  float o[HO::ROWS];
-#pragma unroll
-  for (int k = 0; k < HO::ROWS; ++k) {      // x - (r + l)/2, one rounding
-    const int p = tl.base + HO::row(k);
-    const float xv = in_range(p, L) ? tl.x[p] : 0.f;
-    o[k] = (float)((double)xv - (parked_row<MODE_H8, NBK>(tl, y, n, k, H, T) + (double)lrow[HO::row(k)]) * 0.5);
-  }
-  store_out<MODE_H8, NBK>(tl, y, n, o, H, T);
-}
+namespace hyb640 {
+#define PPNS h16x
+#define HNBK 5
+#include "rrcdnet_hybrid.hpp"
+#undef PPNS
+#undef HNBK
+}  // namespace hyb640
+namespace hyb256 {
+#define PPNS h16xs
+#define HNBK 2
+#include "rrcdnet_hybrid.hpp"
+#undef PPNS
+#undef HNBK
+}  // namespace hyb256
 
 // RDN_F16MIX RRCDNet: hybrid bodies on 640-row tiles, the in-place body on short last tiles
 template <int TAIL>
@@ -277,23 +213,23 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restr
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
   const int need = L - tl.base + 2;
-  if (tl.base >= 0 && tl.base + TileGeo<5>::WB <= L) rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles);
+  if (tl.base >= 0 && tl.base + TileGeo<5>::WB <= L) hyb640::rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles);
   else if (need <= 256) rrcdnet_body<MODE_H8, true, 2, TAIL>(tl, y, n, L, T);
   else if (need <= 384) rrcdnet_body<MODE_H8, true, 3, TAIL>(tl, y, n, L, T);
   else if (need <= 512) rrcdnet_body<MODE_H8, true, 4, TAIL>(tl, y, n, L, T);
-  else rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles);
+  else hyb640::rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles);
 }
 
-// RDN_F16MIX RRCDNet on 256-row tiles (the in-place body, both heads split): the latency geometry for
-// launches too small to fill the chip (launch_fused_inplace_short)
+// RDN_F16MIX RRCDNet on 256-row tiles (the hybrid body on h16xs + the 2-block in-place tile): the
+// latency geometry for launches too small to fill the chip (launch_fused_inplace_short)
 template <int TAIL>
 __global__ __launch_bounds__(THREADS) void rrcdnet_short(const uint8_t* __restrict__ blob, const float* __restrict__ x,
                                                          float* __restrict__ y, int L, int T, int tiles) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
-  if (tl.base >= 0 && tl.base + TileGeo<2>::WB <= L) rrcdnet_body<MODE_H8, false, 2, TAIL>(tl, y, n, L, T);
-  else rrcdnet_body<MODE_H8, true, 2, TAIL>(tl, y, n, L, T);
+  if (tl.base >= 0 && tl.base + TileGeo<2>::WB <= L) hyb256::rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles);
+  else hyb256::rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles);
 }
 
 #define IP_KERNEL(name, arch)                                                                              \

@@ -69,8 +69,8 @@ typedef enum {
  *              last four layers and head on the in-place tile.  The corrected layers are compiled in;
  *              rdn_get_correction_mask reads them back from a packed blob.
  * RDN_F16 / RDN_F16MIX launches that would occupy at most half the CUs with 640-row tiles (e.g. one
- * spectrum per call, evaulate.py:29-32) run on 256-row tiles (same arithmetic; RDN_F16MIX then runs
- * every layer on the in-place tile); the environment variable RDN_SHORT_TILES=0/1 forces either. */
+ * spectrum per call, evaulate.py:29-32) run on 256-row tiles (same arithmetic and, for RDN_F16MIX, the
+ * same hybrid composition); the environment variable RDN_SHORT_TILES=0/1 forces either. */
 typedef enum { RDN_F32 = 0, RDN_BF16 = 1, RDN_BF16X3 = 2, RDN_F16F8 = 3, RDN_F16 = 4, RDN_F16MIX = 5 } rdn_dtype;
 
 enum {
