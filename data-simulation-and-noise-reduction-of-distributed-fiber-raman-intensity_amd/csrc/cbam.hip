@@ -1012,7 +1012,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
     const int c = tid & 63, part = tid >> 6;
     double sp = 0.0;
     unsigned mp = 0;
-    constexpr int PER = 4;
+    constexpr int PER = 2;                 // 16 slots per batch (TT = 16 at L = 10,000)
     for (int t0 = part; t0 < ta.TT; t0 += h16c::WAVES * PER) {
       typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
       u32x2 sv[PER];
