@@ -42,6 +42,10 @@ SA_CONVS = {"ADSDN": 17, "APIDN": 15}
 MFMA_COST = {"f16": 1, "f16-plain": 1, "bf16-unsafe": 1, "bf16x3": 3, "f16f8": 2}
 
 
+# BASELINE.json configs[i] each network's throughput is quoted on
+CONFIG_OF = {"DenoiseCNN": 1, "RRCDNet": 2, "DSDN": 3, "ADSDN": 3, "PIDN": 4, "APIDN": 4}
+
+
 def mfma_cost(arch, dtype):
     """bf16-MFMA units executed per algorithmic product: RDN_F16MIX (Python 'f16' on RRCDNet) runs 3 of
     its 29 big layers with the e4m3 correction (2 units) and the rest plain (1)."""
@@ -98,17 +102,18 @@ def cpu_baseline(arch, L, seconds):
     the reference by the golden fixtures), in the evaulate.py:29-37 loop shape on the box's host cores:
     batch-1 forwards without metrics (`value`), batch-1 with the per-spectrum metrics of
     evaulate.py:34-37 (oracle.metrics: MSE, skimage-0.18.3 SSIM, Smoothness, Peak2Peak), and a
-    batched-16 forward loop (BASELINE.md CPU-baseline plan).  Bounded: ~`seconds` per variant."""
+    batched-16 forward loop (BASELINE.md CPU-baseline plan), at torch.set_num_threads(os.cpu_count())
+    as BASELINE.md prescribes; the batch-1 loop also at 16 threads (the GPU box's CPU share: its
+    os.cpu_count() reports the whole host).  Bounded: ~`seconds` per variant."""
     from oracle.metrics import per_spectrum
     from oracle.models import forward as oracle_forward
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    all_threads = os.cpu_count() or 1
     sd, wsrc = _weights(arch)
     clean, noisy = _reference_inputs(64, L)
     xs = [torch.tensor(v, dtype=torch.float32).view(1, 1, -1) for v in noisy]
-    oracle_forward(arch, sd, xs[0])                  # warm-up
 
     def loop(body):
+        body(0)                                              # warm-up
         n, t0 = 0, time.perf_counter()
         while True:
             body(n)
@@ -117,18 +122,32 @@ def cpu_baseline(arch, L, seconds):
             if el >= seconds and n >= 3:
                 return n, el
 
+    torch.set_num_threads(all_threads)
     n1, e1 = loop(lambda i: oracle_forward(arch, sd, xs[i % len(xs)]))
     n2, e2 = loop(lambda i: per_spectrum(oracle_forward(arch, sd, xs[i % len(xs)]).view(1, -1).numpy(),
                                          clean[i % len(xs)][None]))
     xb = torch.tensor(noisy[:16], dtype=torch.float32).unsqueeze(1)
     n3, e3 = loop(lambda i: oracle_forward(arch, sd, xb))
-    return {"value": n1 / e1, "unit": "spectra/s", "cores": threads, "kind": "port",
+    t16 = min(16, all_threads)
+    torch.set_num_threads(t16)
+    n4, e4 = loop(lambda i: oracle_forward(arch, sd, xs[i % len(xs)]))
+    torch.set_num_threads(all_threads)
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = None
+    return {"value": n1 / e1, "unit": "spectra/s", "cores": all_threads, "kind": "port",
             "sample": f"{n1} batch-1 fp32 {arch} forwards at L={L} ({e1:.1f} s), evaulate.py:29-32 loop shape, "
-                      f"oracle.models (the reference's ops) on {threads} threads; weights: {wsrc}; inputs: the "
-                      "reference generator (oracle.refgen, seed 20250410)",
+                      f"oracle.models (the reference's ops) at torch.set_num_threads(os.cpu_count() = {all_threads}); "
+                      f"weights: {wsrc}; inputs: the reference generator (oracle.refgen, seed 20250410)",
             "with_metrics_spectra_per_s": n2 / e2,
             "batched16_spectra_per_s": 16 * n3 / e3,
-            "host": {"cpu_model": _cpu_model_name(), "os_cpu_count": os.cpu_count(), "torch": torch.__version__}}
+            "threads16_spectra_per_s": n4 / e4,
+            "note": "batched-16 runs the oracle's functional forward on a (16,1,L) tensor: one oneDNN conv per layer "
+                    "over 16x the data, slower per spectrum than batch 1 on this host (cache-resident batch-1 "
+                    "activations: 64 x L x 4 B = 2.6 MB per layer vs 41 MB at batch 16)",
+            "host": {"cpu_model": _cpu_model_name(), "os_cpu_count": all_threads, "sched_affinity_cpus": avail,
+                     "torch": torch.__version__}}
 
 
 def batch1_latency(model, code, arch, L, dev, n=200):
@@ -182,9 +201,10 @@ def time_forward(engine, arch, dtype, packed, x, y, steps, warmup, stream):
 
 def time_pipeline(engine, arch, dtype, packed, seed, first, B, L, steps, stream, dev):
     """SURVEY.md §8d configs 3-4 end to end, reported beside `value` (never as it): per step the
-    device simulator writes B fresh spectra (new indices each step), the fused forward denoises them
-    and the fp64 metric kernel accumulates the evaluate sums (evaulate.py:29-39) — no host sync,
-    nothing leaves HBM.  Also times each stage alone on the same buffers."""
+    device simulator writes B fresh spectra (indices first + i*B, i = 0..steps: the caller gives each
+    rank a disjoint block of (steps + 1) * B indices), the fused forward denoises them and the fp64
+    metric kernel accumulates the evaluate sums (evaulate.py:29-39) — no host sync, nothing leaves
+    HBM.  Also times each stage alone on the same buffers."""
     clean = torch.empty((B, L), dtype=torch.float32, device=dev)
     noisy = torch.empty((B, L), dtype=torch.float32, device=dev)
     y = torch.empty((B, 1, L), dtype=torch.float32, device=dev)
@@ -221,6 +241,85 @@ def time_pipeline(engine, arch, dtype, packed, seed, first, B, L, steps, stream,
             "note": "simulate -> fused forward -> fp64 metric sums per step, all on device (configs 3-4)"}
 
 
+def _model(R, arch, dtype, dev, trained=True):
+    """Module of `arch` on `dev` with the trained golden fixture weights (or random init)."""
+    torch.manual_seed(1234)
+    m = R.MODELS[arch]()
+    src = "random init"
+    if trained:
+        sd, src = _weights(arch)
+        m.load_state_dict(sd, strict=True)
+    return m.to(dev).eval().set_engine_dtype(dtype), src
+
+
+def config_keys(R, engine, args, dev, stream, world, rank):
+    """BASELINE.json configs 2, 4 and 5 as extra keys of the bench line (each labelled with its own
+    configs[i]), on the trained golden fixture weights.  Config 4 runs at every world size (the
+    data-parallel driver: rank r owns [r*N/W, (r+1)*N/W), exact metric sums all-reduced, so its means
+    are identical for any W); configs 2 and 5 are single-GPU configurations (rank 0 of a 1-GPU run)."""
+    from raman_mi355x.evaluate import evaluate_synthetic
+    out = {}
+    L = args.L
+    # config 4: RRCDNet + DSDN/ADSDN data-parallel, fixed total N (evaluate_synthetic)
+    B4 = args.config4_batch
+    total = world * args.config4_chunks * B4
+    models = {a: _model(R, a, args.dtype, dev)[0] for a in args.config4_archs.split(",")}
+    evaluate_synthetic({a: m for a, m in models.items()}, world * 2, seed=args.seed, signal_length=L,
+                       batch_size=2, device=dev)                                   # warm-up (pack, first launch)
+    res = evaluate_synthetic(models, total, seed=args.seed, signal_length=L, batch_size=B4, device=dev)
+    cfg4 = {"config": "BASELINE.json configs[3]", "total_spectra": total, "batch_per_gpu": B4,
+            "dtype": args.dtype, "signal_length": L, "n_gpus": world,
+            "note": "evaluate_synthetic: per chunk on-device simulate -> fused forward -> exact metric sums; rank r "
+                    "owns spectrum indices [r*N/W, (r+1)*N/W); the accumulators are all-reduced once (means "
+                    "identical for any W); CBAM hand-off status checked once per network"}
+    for a, r in res.items():
+        sps = r["spectra_per_s"]
+        cfg4[a] = {"spectra_per_s": sps, "seconds": r["seconds"], "means": r["means"], "engine_dtype_code": models[a].engine_code,
+                   "roofline_frac_per_gpu": flops_per_spectrum(a, L) * sps / world / 1e12 / PEAK_TFLOPS[args.dtype]}
+    out["config4"] = cfg4
+    if world > 1 or rank != 0:
+        return out
+    # config 2: 1DCNN fp32 on config2_n on-device spectra
+    m2, src = _model(R, "DenoiseCNN", "fp32", dev)
+    evaluate_synthetic({"DenoiseCNN": m2}, 4, seed=args.seed, signal_length=L, batch_size=4, device=dev)
+    r2 = evaluate_synthetic({"DenoiseCNN": m2}, args.config2_n, seed=args.seed, signal_length=L,
+                            batch_size=args.config2_batch, device=dev)["DenoiseCNN"]
+    x2 = engine.generate(args.config2_batch, args.seed, signal_length=L, device=dev)[1].view(-1, 1, L)
+    ms2 = time_forward(engine, "DenoiseCNN", m2.engine_code, m2.packed_weights(dev), x2, torch.empty_like(x2), 3, 1, stream)
+    del x2
+    out["config2"] = {"config": "BASELINE.json configs[1]", "arch": "DenoiseCNN", "dtype": "fp32",
+                      "spectra": args.config2_n, "signal_length": L, "weights": src,
+                      "spectra_per_s": r2["spectra_per_s"], "seconds": r2["seconds"], "means": r2["means"],
+                      "forward_kernel_ms": ms2, "forward_batch": args.config2_batch,
+                      "roofline_frac": flops_per_spectrum("DenoiseCNN", L) * args.config2_batch / (ms2 * 1e-3) / 1e12
+                      / PEAK_TFLOPS["fp32"],
+                      "note": "end to end (simulate -> forward -> metrics) over all spectra; roofline_frac from the "
+                              "forward kernel alone (HIP events)"}
+    # config 5: PIDN / APIDN at L = 16384, 'f16' and fp32, plus the f16-vs-fp32 gap on the same inputs
+    L5 = 16384
+    cfg5 = {"config": "BASELINE.json configs[4]", "signal_length": L5}
+    for a in ("PIDN", "APIDN"):
+        nb = {"PIDN": 2500, "APIDN": 1250}[a]
+        x5 = engine.generate(nb, args.seed, first_index=10 ** 9, signal_length=L5, device=dev)[1].view(nb, 1, L5)
+        y5 = torch.empty_like(x5)
+        rec = {}
+        outs = {}
+        for dt, n in (("f16", nb), ("fp32", nb // 4)):
+            m5, src = _model(R, a, dt, dev)
+            pk = m5.packed_weights(dev)
+            ms = time_forward(engine, a, m5.engine_code, pk, x5[:n], y5[:n], 3, 1, stream)
+            ws = engine.Workspace(a, m5.engine_code, 64, L5, dev) if a in engine.CBAM_ARCHS else None
+            outs[dt] = engine.forward(a, m5.engine_code, pk, x5[:64], check=True, workspace=ws).cpu()
+            rec[dt] = {"spectra_per_s": n / (ms * 1e-3), "kernel_ms": ms, "batch": n,
+                       "roofline_frac": flops_per_spectrum(a, L5) * n / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[dt]}
+        rec["f16_vs_fp32_max_abs_64_spectra"] = float((outs["f16"] - outs["fp32"]).abs().max())
+        rec["weights"] = src
+        cfg5[a] = rec
+        del x5, y5
+    out["config5"] = cfg5
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -237,6 +336,14 @@ def main():
     ap.add_argument("--no-batch1", action="store_true", help="skip the batch-1 evaluate-loop latency")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip timing the simulate -> forward -> metrics pipeline (SURVEY.md §8d configs 3-4)")
+    ap.add_argument("--no-configs", action="store_true", help="skip the configs 2/4/5 keys")
+    ap.add_argument("--config2-n", type=int, default=1_000_000, help="config 2 spectra (1DCNN fp32)")
+    ap.add_argument("--config2-batch", type=int, default=65536)
+    ap.add_argument("--config4-batch", type=int, default=8192)
+    ap.add_argument("--config4-chunks", type=int, default=4, help="config 4 chunks per rank")
+    ap.add_argument("--config4-archs", default="RRCDNet,DSDN,ADSDN",
+                    help="(ranks sharing one GPU under gloo must leave out the CBAM networks: their team "
+                         "kernel assumes the whole device)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI, one rank per GPU); gloo rehearses the N>1 path with ranks "
                          "sharing the visible GPUs (collectives staged through host memory)")
@@ -245,10 +352,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    gloo = world > 1 and args.dist_backend == "gloo"
+    # launched by torch.distributed.run (WORLD_SIZE set, even at 1): a process group over RCCL ("nccl")
+    # or gloo; a plain `python bench.py` runs without one
+    distributed = "WORLD_SIZE" in os.environ
+    gloo = distributed and args.dist_backend == "gloo"
     if gloo:
         local = local % torch.cuda.device_count()
-    if world > 1:
+    if distributed:
         torch.cuda.set_device(local)
         if gloo:
             dist.init_process_group("gloo")
@@ -284,7 +394,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -294,13 +404,13 @@ def main():
         step()
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps      # one fused kernel launch per step
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if distributed:
         all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
@@ -309,7 +419,7 @@ def main():
         raise RuntimeError("non-finite outputs in the timed forward")
     # evaluation metrics of the last step, all-reduced across ranks (RCCL over xGMI) — untimed
     _, sums = engine.metrics(y.view(B, L), clean)
-    if world > 1:
+    if distributed:
         all_reduce(sums)
     sums = sums.cpu().tolist()
 
@@ -325,14 +435,30 @@ def main():
                             "roofline_frac": flops_per_spectrum(args.arch, L) * nb / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[dt]}
         model.set_engine_dtype(args.dtype)
 
+    # the headline kernel on the trained golden fixture weights (the clock the chip holds depends on
+    # the operands: MI355X_MICROARCH.md DVFS give-back), beside the random-init `value`
+    trained = None
+    if not args.no_variants:
+        mt, tsrc = _model(R, args.arch, args.dtype, dev)
+        ms = time_forward(engine, args.arch, mt.engine_code, mt.packed_weights(dev), x, y, max(3, args.steps // 4), 1, stream)
+        trained = {"spectra_per_s_per_gpu": B / (ms * 1e-3), "kernel_ms": ms, "batch": B, "weights": tsrc,
+                   "roofline_frac": flops_per_spectrum(args.arch, L) * B / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[args.dtype]}
+        del mt
+
     batch1 = None
     if not args.no_batch1 and rank == 0:
         batch1 = batch1_latency(model, code, args.arch, L, dev)
 
     pipeline = None
     if not args.no_pipeline:
-        pipeline = time_pipeline(engine, args.arch, code, packed, args.seed, (world + rank) * B, B, L,
+        # indices [0, world*B) fed the headline; each rank's pipeline block of 4*B indices follows,
+        # disjoint across ranks (rank r once re-generated rank r+1's steps)
+        pipeline = time_pipeline(engine, args.arch, code, packed, args.seed, world * B + rank * 4 * B, B, L,
                                  3, stream, dev)
+
+    configs = None
+    if not args.no_configs:
+        configs = config_keys(R, engine, args, dev, stream, world, rank)
 
     if rank == 0:
         total = world * B * args.steps
@@ -346,7 +472,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (on-device simulator, 数据集产生.py contract; random-init weights)",
             "config": {"workload": f"{args.arch} {args.dtype} fused forward, on-device simulator inputs "
-                                   "(BASELINE.json configs[2])", "engine_dtype_code": code,
+                                   f"(BASELINE.json configs[{CONFIG_OF[args.arch]}])", "engine_dtype_code": code,
                        "arch": args.arch, "signal_length": L, "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"dp{world}", **({"dist_backend": "gloo (rehearsal)"} if gloo else {})},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
@@ -357,14 +483,16 @@ def main():
                          "executed_bf16_equiv_tflops": (achieved * mfma_cost(args.arch, args.dtype)
                                                         if mfma_cost(args.arch, args.dtype) else None)},
             "variants": variants,
+            "trained_weights": trained,
             "pipeline": pipeline,
+            "configs": configs,
             "batch1": batch1,
             "metrics_mean": {k: sums[i] / sums[4] for i, k in enumerate(["MSE", "SSIM", "Smoothness", "Peak2Peak"])},
         }
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(args.arch, L, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

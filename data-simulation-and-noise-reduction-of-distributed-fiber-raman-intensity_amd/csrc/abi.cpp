@@ -1,6 +1,7 @@
 // C ABI (include/raman_mi355x.h): argument checking, error reporting and dispatch.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -16,6 +17,7 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
 size_t packed_bytes(const std::vector<Op>& spec, int dtype);
 void set_corr_mask(void* blob, uint64_t mask);
 uint64_t get_corr_mask(const void* blob);
+uint32_t get_blob_tag(const void* blob);
 uint64_t f16mix_default_mask(int arch);
 hipError_t launch_fused16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
 hipError_t launch_fused16_f16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
@@ -29,9 +31,11 @@ hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const f
                                void* ws, size_t ws_bytes, hipStream_t s);
 size_t cbam_workspace_bytes(int arch, int dtype, int64_t n, int64_t L, hipStream_t s);
 hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t s, int* timed_out);
+hipError_t cbam_workspace_init(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t s);
 hipError_t launch_generate(uint64_t seed, uint64_t first, int64_t n, int L, float snr_lo, float snr_hi, float extreme_prob,
                            int max_repeat, float* clean, float* noisy, float* snr, float* nstd, hipStream_t s);
-hipError_t launch_metrics(const float* y, const float* clean, int64_t n, int L, double* per, double* sums, hipStream_t s);
+hipError_t launch_metrics(const float* y, const void* clean, bool clean_f64, int64_t n, int L, double* per, double* sums,
+                          long long* acc, hipStream_t s);
 }  // namespace rdn
 
 namespace {
@@ -51,6 +55,14 @@ int hip_check(hipError_t e, const char* what) {
 bool valid_arch(int a) { return a >= RDN_DENOISECNN && a <= RDN_APIDN; }
 bool valid_dtype(int d) { return d >= RDN_F32 && d <= RDN_F16MIX; }
 bool is_cbam(int a) { return a == RDN_ADSDN || a == RDN_APIDN; }
+// RDN_F16MIX exists for RRCDNet only (checked before any per-network dispatch)
+bool unsupported(int arch, int dtype) { return dtype == RDN_F16MIX && arch != RDN_RRCDNET; }
+int fail_unsupported(const char* fn) {
+  return fail(RDN_EUNSUPPORTED, std::string(fn) + ": RDN_F16MIX is built for RRCDNet; the other networks run RDN_F16");
+}
+
+static_assert(rdn::BLOB_MAGIC == RDN_BLOB_MAGIC, "blob tag magic");
+static_assert(sizeof(long long) == sizeof(int64_t), "accumulator words");
 
 }  // namespace
 
@@ -117,6 +129,24 @@ int rdn_pack(int arch, int dtype, const float* const* tensors, const int64_t* nu
   RDN_GUARD_END
 }
 
+int rdn_check_blob(int arch, int dtype, const void* host_blob, size_t bytes) {
+  RDN_GUARD_BEGIN
+  if (!valid_arch(arch) || !valid_dtype(dtype) || !host_blob) return fail(RDN_EINVAL, "rdn_check_blob: bad argument");
+  if (unsupported(arch, dtype)) return fail_unsupported("rdn_check_blob");
+  const size_t need = rdn::packed_bytes(rdn::net_spec(arch), dtype);
+  if (bytes < need) return fail(RDN_ESIZE, "rdn_check_blob: blob of " + std::to_string(bytes) + " bytes, the layout needs " +
+                                               std::to_string(need));
+  const uint32_t tag = rdn::get_blob_tag(host_blob);
+  if (tag != rdn::blob_tag(arch, dtype)) {
+    if ((tag & 0xffff0000u) != RDN_BLOB_MAGIC) return fail(RDN_EINVAL, "rdn_check_blob: not an rdn_pack blob (no layout tag)");
+    return fail(RDN_EINVAL, "rdn_check_blob: blob packed for arch " + std::to_string((tag >> 8) & 0xff) + " dtype " +
+                                std::to_string(tag & 0xff) + ", not arch " + std::to_string(arch) + " dtype " +
+                                std::to_string(dtype));
+  }
+  return RDN_OK;
+  RDN_GUARD_END
+}
+
 int rdn_default_correction_mask(int arch, uint64_t* mask) {
   RDN_GUARD_BEGIN
   if (!valid_arch(arch) || !mask) return fail(RDN_EINVAL, "rdn_default_correction_mask: bad argument");
@@ -130,18 +160,34 @@ int rdn_get_correction_mask(int arch, int dtype, const void* host_blob, size_t b
   if (!valid_arch(arch) || !valid_dtype(dtype) || !host_blob || !mask)
     return fail(RDN_EINVAL, "rdn_get_correction_mask: bad argument");
   if (dtype != RDN_F16F8 && dtype != RDN_F16MIX) return fail(RDN_EINVAL, "rdn_get_correction_mask: not a correction layout");
-  if (bytes < rdn::packed_bytes(rdn::net_spec(arch), dtype)) return fail(RDN_ESIZE, "rdn_get_correction_mask: blob too small");
+  const int chk = rdn_check_blob(arch, dtype, host_blob, bytes);
+  if (chk != RDN_OK) return chk;
   *mask = rdn::get_corr_mask(host_blob);
   return RDN_OK;
   RDN_GUARD_END
 }
 
-int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes) {
+int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes, void* stream) {
   RDN_GUARD_BEGIN
   if (!valid_arch(arch) || !valid_dtype(dtype) || !bytes || n < 0 || L < 1)
     return fail(RDN_EINVAL, "rdn_workspace_size: bad argument");
-  *bytes = is_cbam(arch) ? rdn::cbam_workspace_bytes(arch, dtype, n, L, nullptr) : 0;
+  if (unsupported(arch, dtype)) return fail_unsupported("rdn_workspace_size");
+  *bytes = is_cbam(arch) ? rdn::cbam_workspace_bytes(arch, dtype, n, L, (hipStream_t)stream) : 0;
   return RDN_OK;
+  RDN_GUARD_END
+}
+
+int rdn_workspace_init(int arch, int dtype, int64_t n, int64_t L, void* ws, size_t ws_bytes, void* stream) {
+  RDN_GUARD_BEGIN
+  if (!valid_arch(arch) || !valid_dtype(dtype) || n < 0 || L < 1 || L > 0x7fffffff)
+    return fail(RDN_EINVAL, "rdn_workspace_init: bad argument");
+  if (unsupported(arch, dtype)) return fail_unsupported("rdn_workspace_init");
+  if (!is_cbam(arch)) return RDN_OK;
+  const hipStream_t s = (hipStream_t)stream;
+  const size_t need = rdn::cbam_workspace_bytes(arch, dtype, n, L, s);
+  if (ws_bytes < need || (need && !ws))
+    return fail(RDN_ESIZE, "rdn_workspace_init: workspace too small, need " + std::to_string(need) + " bytes");
+  return hip_check(rdn::cbam_workspace_init(arch, dtype, L, ws, ws_bytes, s), "rdn_workspace_init");
   RDN_GUARD_END
 }
 
@@ -168,6 +214,7 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
     const uintptr_t xb = (uintptr_t)x, yb = (uintptr_t)y, bytes = (uintptr_t)(n * L) * sizeof(float);
     if (xb < yb + bytes && yb < xb + bytes) return fail(RDN_EINVAL, "rdn_forward: x and y overlap");
   }
+  if (unsupported(arch, dtype)) return fail_unsupported("rdn_forward");
   const hipStream_t s = (hipStream_t)stream;
   const uint8_t* blob = (const uint8_t*)packed;
   if (is_cbam(arch)) {
@@ -181,8 +228,6 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
   if (dtype == RDN_F16)
     return hip_check(shrt ? rdn::launch_fused16_f16_small(arch, blob, x, y, n, (int)L, s)
                           : rdn::launch_fused16_f16(arch, blob, x, y, n, (int)L, s), "fused f16 forward");
-  if (dtype == RDN_F16MIX && arch != RDN_RRCDNET)
-    return fail(RDN_EUNSUPPORTED, "RDN_F16MIX is built for RRCDNet; the other networks run RDN_F16");
   if (dtype == RDN_F16MIX && shrt)
     return hip_check(rdn::launch_fused_inplace_short(blob, x, y, n, (int)L, s), "fused f16mix forward (short tiles)");
   return hip_check(rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, s), "fused in-place forward");
@@ -193,8 +238,13 @@ int rdn_forward_status(int arch, int dtype, int64_t n, int64_t L, void* ws, size
   RDN_GUARD_BEGIN
   if (!valid_arch(arch) || !valid_dtype(dtype)) return fail(RDN_EINVAL, "rdn_forward_status: unknown arch/dtype");
   if (n < 0 || L < 1 || L > 0x7fffffff) return fail(RDN_EINVAL, "rdn_forward_status: bad n / L");
+  if (unsupported(arch, dtype)) return fail_unsupported("rdn_forward_status");
   const hipStream_t s = (hipStream_t)stream;
   if (!is_cbam(arch) || n == 0) return hip_check(hipStreamSynchronize(s), "rdn_forward_status");
+  const size_t need = rdn::cbam_workspace_bytes(arch, dtype, n, L, s);
+  if (ws_bytes < need || (need && !ws))
+    return fail(RDN_ESIZE, "rdn_forward_status: workspace smaller than this device's CBAM geometry needs (" +
+                               std::to_string(need) + " bytes)");
   int timed_out = 0;
   const int rc = hip_check(rdn::cbam_status(arch, dtype, L, ws, ws_bytes, s, &timed_out), "rdn_forward_status");
   if (rc != RDN_OK) return rc;
@@ -226,7 +276,70 @@ int rdn_metrics(const float* y, const float* clean, int64_t n, int64_t L, double
   if (!y || !clean) return fail(RDN_EINVAL, "rdn_metrics: null pointer");
   if (n < 0 || L < 7 || L > 0x7fffffff) return fail(RDN_EINVAL, "rdn_metrics: need L >= 7 (SSIM window)");
   if (n == 0) return RDN_OK;
-  return hip_check(rdn::launch_metrics(y, clean, n, (int)L, per_spectrum, sums, (hipStream_t)stream), "metrics");
+  return hip_check(rdn::launch_metrics(y, clean, false, n, (int)L, per_spectrum, sums, nullptr, (hipStream_t)stream),
+                   "metrics");
+  RDN_GUARD_END
+}
+
+int rdn_metrics_ex(const float* y, const void* clean, int clean_is_f64, int64_t n, int64_t L, double* per_spectrum,
+                   double* sums, int64_t* acc, void* stream) {
+  RDN_GUARD_BEGIN
+  if (!y || !clean) return fail(RDN_EINVAL, "rdn_metrics_ex: null pointer");
+  if (clean_is_f64 != 0 && clean_is_f64 != 1) return fail(RDN_EINVAL, "rdn_metrics_ex: clean_is_f64 must be 0 or 1");
+  if (n < 0 || L < 7 || L > 0x7fffffff) return fail(RDN_EINVAL, "rdn_metrics_ex: need L >= 7 (SSIM window)");
+  if (n == 0) return RDN_OK;
+  return hip_check(rdn::launch_metrics(y, clean, clean_is_f64 == 1, n, (int)L, per_spectrum, sums, (long long*)acc,
+                                       (hipStream_t)stream),
+                   "metrics");
+  RDN_GUARD_END
+}
+
+// Exact accumulator -> doubles: the limbs are carried into base-2^32 digits of the signed total
+// (sign-magnitude after one negation), whose leading 64 bits with a sticky bit for the rest
+// convert to double with one round-to-nearest-even.
+static double acc_to_double(const int64_t* limb) {
+  int64_t l[RDN_ACC_LIMBS];
+  for (int j = 0; j < RDN_ACC_LIMBS; ++j) l[j] = limb[j];
+  auto carry = [&](uint32_t (&d)[RDN_ACC_LIMBS + 2]) {
+    __int128 c = 0;
+    for (int j = 0; j < RDN_ACC_LIMBS; ++j) {
+      const __int128 t = (__int128)l[j] + c;
+      d[j] = (uint32_t)(t & 0xffffffff);
+      c = (t - (__int128)d[j]) / ((__int128)1 << 32);
+    }
+    d[RDN_ACC_LIMBS] = (uint32_t)(c & 0xffffffff);
+    d[RDN_ACC_LIMBS + 1] = (uint32_t)((c >> 32) & 0xffffffff);
+    return c < 0;
+  };
+  uint32_t d[RDN_ACC_LIMBS + 2];
+  bool neg = carry(d);
+  if (neg) {
+    for (int j = 0; j < RDN_ACC_LIMBS; ++j) l[j] = -l[j];
+    carry(d);
+  }
+  int top = RDN_ACC_LIMBS + 1;
+  while (top >= 0 && d[top] == 0) --top;
+  if (top < 0) return 0.0;
+  const int hb = 32 * top + (31 - __builtin_clz(d[top]));     // highest set bit
+  auto bit = [&](int i) -> uint64_t { return i < 0 ? 0 : (d[i >> 5] >> (i & 31)) & 1u; };
+  uint64_t u = 0;
+  const int lo = hb - 63;
+  for (int i = hb; i >= lo; --i) u = (u << 1) | bit(i);
+  bool sticky = false;
+  for (int i = lo - 1; i >= 0 && !sticky; --i) sticky = bit(i);
+  const double v = std::ldexp((double)(u | (sticky ? 1u : 0u)), lo - RDN_ACC_FRAC_BITS);
+  return neg ? -v : v;
+}
+
+int rdn_acc_value(const int64_t* acc, double* sums) {
+  RDN_GUARD_BEGIN
+  if (!acc || !sums) return fail(RDN_EINVAL, "rdn_acc_value: null pointer");
+  for (int k = 0; k < 4; ++k) {
+    const int64_t* a = acc + k * RDN_ACC_STRIDE;
+    sums[k] = a[RDN_ACC_LIMBS] ? std::nan("") : acc_to_double(a);
+  }
+  sums[4] = (double)acc[RDN_ACC_COUNT];
+  return RDN_OK;
   RDN_GUARD_END
 }
 

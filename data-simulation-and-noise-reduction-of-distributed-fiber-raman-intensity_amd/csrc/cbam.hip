@@ -320,7 +320,7 @@ struct TeamArgs {
   char* slots;          // [teams][2][TT][SLOT_BYTES]
   unsigned* counters;   // [teams][TEAM_CTR_STRIDE], zeroed before the launch
   char* hsave;          // [teams * TT][WB][64] f32
-  unsigned* err;         // hand-off error word: set when a team wait times out (read by cbam_status)
+  unsigned* err;         // hand-off error words: [0] this launch (fast-fail, NaN outputs), [1] sticky (cbam_status)
   unsigned long long* stamps;   // RDN_TEAM_STAMPS diagnostics: [grid][NSTAMP] cycle sums per phase
   int force_miss;       // test knob (RDN_CBAM_FORCE_MISS=k): workgroup 0 skips its k-th arrival
 };
@@ -540,6 +540,7 @@ __device__ __forceinline__ void team_wait(const TeamArgs& ta, unsigned* ctr, uns
       if ((++it & 63) == 0 && __hip_atomic_load(ta.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
       if (it > SPIN_LIMIT) {
         __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ta.err + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sticky word
         break;
       }
     }
@@ -1358,7 +1359,8 @@ static hipError_t launch_team(int arch, int mode, const TeamGeo& g, const uint8_
   const char* miss = getenv("RDN_CBAM_FORCE_MISS");     // test knob: see TeamArgs::force_miss
   ta.force_miss = miss ? atoi(miss) : 0;
   ta.stamps = cb::STAMP_BYTES ? (unsigned long long*)((char*)ws + g.total - cb::STAMP_BYTES) : nullptr;
-  // counters and the error word start at 0 (the hand-off counts arrivals monotonically)
+  // counters and this launch's error word start at 0 (the hand-off counts arrivals monotonically);
+  // the sticky word after it collects every launch's timeouts until cbam_status reads and clears it
   hipError_t e = hipMemsetAsync(ta.counters, 0, g.counters, stream);
   if (e == hipSuccess) e = hipMemsetAsync(ta.err, 0, 4, stream);
   if (e != hipSuccess) return e;
@@ -1461,19 +1463,30 @@ hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const f
   return hipSuccess;
 }
 
-// After a CBAM forward on `stream`: wait for it and read the team kernel's hand-off error word.
-// *timed_out = 1 if a team wait exceeded its spin limit (outputs of affected spectra are NaN).
+// A new workspace: clear the team kernel's sticky hand-off error word (the caller checked the size).
+hipError_t cbam_workspace_init(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t stream) {
+  const TeamGeo tg = team_geo(arch, team_mode(dtype), L, stream_device(stream));
+  if (tg.teams <= 0) return hipSuccess;                                 // segment path: no hand-off
+  if (!ws || ws_bytes < tg.total) return hipErrorInvalidValue;
+  return hipMemsetAsync(team_err(tg, ws) + 1, 0, 4, stream);          // the sticky word
+}
+
+// After CBAM forwards on `stream`: wait for them, then read and clear the team kernel's sticky
+// hand-off error word.  *timed_out = 1 if a team wait of any forward since the last read exceeded
+// its spin limit (outputs of affected spectra are NaN).  The caller checked the workspace size.
 hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t stream, int* timed_out) {
   *timed_out = 0;
   hipError_t e = hipStreamSynchronize(stream);
   if (e != hipSuccess) return e;
   const TeamGeo tg = team_geo(arch, team_mode(dtype), L, stream_device(stream));
-  if (tg.teams <= 0 || !ws || ws_bytes < tg.total) return hipSuccess;   // segment path: no hand-off
+  if (tg.teams <= 0) return hipSuccess;                                 // segment path: no hand-off
+  if (!ws || ws_bytes < tg.total) return hipErrorInvalidValue;
   unsigned err = 0;
-  e = hipMemcpy(&err, team_err(tg, ws), sizeof(err), hipMemcpyDeviceToHost);
+  e = hipMemcpy(&err, team_err(tg, ws) + 1, sizeof(err), hipMemcpyDeviceToHost);     // the sticky word
   if (e != hipSuccess) return e;
   *timed_out = err != 0;
-  return hipSuccess;
+  if (err) e = hipMemset(team_err(tg, ws) + 1, 0, 4);
+  return e;
 }
 
 }  // namespace rdn

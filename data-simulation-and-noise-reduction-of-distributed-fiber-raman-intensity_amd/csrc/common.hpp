@@ -35,6 +35,11 @@ constexpr size_t SMALL_BYTES = SMALL_SLOTS * SMALL_SLOT_FLOATS * sizeof(float); 
 // slot 63 word 0/1: 64-bit per-layer correction mask of the f16 + e4m3 layout (bit i = big layer i
 // consumes the e4m3 correction): all ones for RDN_F16F8, a calibrated subset for RDN_F16MIX
 constexpr int CORR_SLOT = 63;
+// slot 63 word 2: layout tag BLOB_MAGIC | arch << 8 | dtype, written by rdn_pack for every dtype
+// (include/raman_mi355x.h RDN_BLOB_MAGIC); the RDN_F16MIX kernels check it before reading the blob
+constexpr uint32_t BLOB_MAGIC = 0x52440000u;
+constexpr int TAG_WORD = 2;
+__host__ __device__ constexpr uint32_t blob_tag(int arch, int dtype) { return BLOB_MAGIC | (uint32_t)arch << 8 | (uint32_t)dtype; }
 // bf16 big layer: A-fragments of v_mfma_f32_16x16x32_bf16, [m 4][kstep 6][lane 64][8 bf16],
 // lane l holds W[cout = 16m + (l&15)][cin = 32u + 8(l>>4) + j][tap t], kstep = 2t + u; then bias[64] f32.
 constexpr int BIG_FRAG_BYTES_BF16 = 4 * 6 * 64 * 16;                       // 24576

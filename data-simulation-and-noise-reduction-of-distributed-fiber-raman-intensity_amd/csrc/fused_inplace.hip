@@ -205,6 +205,19 @@ namespace hyb256 {
 #undef HNBK
 }  // namespace hyb256
 
+// RDN_F16MIX reads one record past an RDN_F16F8 blob's end: a blob whose layout tag (pack.cpp) is not
+// RDN_F16MIX RRCDNet's gets NaN outputs instead of a read past it (one scalar load per workgroup)
+__device__ __forceinline__ bool f16mix_blob_ok(const uint8_t* blob) {
+  const uint32_t tag = ((const __attribute__((address_space(4))) uint32_t*)blob)[CORR_SLOT * SMALL_SLOT_FLOATS + TAG_WORD];
+  return tag == blob_tag(RRCDNET, F16MIX);
+}
+__device__ __forceinline__ void nan_outputs(const Tile& tl, float* y, int n, int T) {
+  for (int j = __builtin_amdgcn_workitem_id_x(); j < T; j += THREADS) {
+    const int p = tl.base + fused_halo(RRCDNET) + j;
+    if (p < tl.L) y[(size_t)n * tl.L + p] = __uint_as_float(0x7fc00000u);
+  }
+}
+
 // RDN_F16MIX RRCDNet: hybrid bodies on 640-row tiles, the in-place body on short last tiles
 template <int TAIL>
 __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restrict__ blob, const float* __restrict__ x,
@@ -212,6 +225,7 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restr
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
+  if (!f16mix_blob_ok(blob)) return nan_outputs(tl, y, n, T);
   const int need = L - tl.base + 2;
   if (tl.base >= 0 && tl.base + TileGeo<5>::WB <= L) hyb640::rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles);
   else if (need <= 256) rrcdnet_body<MODE_H8, true, 2, TAIL>(tl, y, n, L, T);
@@ -228,6 +242,7 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_short(const uint8_t* __restri
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
+  if (!f16mix_blob_ok(blob)) return nan_outputs(tl, y, n, T);
   if (tl.base >= 0 && tl.base + TileGeo<2>::WB <= L) hyb256::rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles);
   else hyb256::rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles);
 }

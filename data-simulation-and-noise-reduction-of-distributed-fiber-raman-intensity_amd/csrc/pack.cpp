@@ -551,7 +551,12 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
     }
   }
   if (dtype == F16F8 || dtype == F16MIX) set_corr_mask(out, dtype == F16F8 ? ~0ull : f16mix_default_mask(arch));
+  ((uint32_t*)(out + (size_t)CORR_SLOT * SMALL_SLOT_FLOATS * 4))[TAG_WORD] = blob_tag(arch, dtype);
   return "";
+}
+
+uint32_t get_blob_tag(const void* blob) {
+  return ((const uint32_t*)((const uint8_t*)blob + (size_t)CORR_SLOT * SMALL_SLOT_FLOATS * 4))[TAG_WORD];
 }
 
 // RDN_F16MIX: the big layers (execution order) that keep the e4m3 correction.  Plain f16 (RDN_F16)

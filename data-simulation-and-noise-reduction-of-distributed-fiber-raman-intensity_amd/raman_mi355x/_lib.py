@@ -18,7 +18,13 @@ CSRC = os.path.join(os.path.dirname(PKG), "csrc")
 HEADER = os.path.join(os.path.dirname(os.path.dirname(PKG)), "include", "raman_mi355x.h")
 
 RDN_OK = 0
-ABI_VERSION = 2
+ABI_VERSION = 3
+# exact metric accumulator words (include/raman_mi355x.h RDN_ACC_*)
+ACC_LIMBS = 6
+ACC_STRIDE = ACC_LIMBS + 1
+ACC_COUNT = 4 * ACC_STRIDE
+ACC_WORDS = ACC_COUNT + 1
+ACC_FRAC_BITS = 128
 
 
 def source_hash():
@@ -58,13 +64,19 @@ _SIGNATURES = {
     "rdn_pack": ([ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
                   ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t], ctypes.c_int),
     "rdn_workspace_size": ([ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
-                            ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+                            ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p], ctypes.c_int),
+    "rdn_workspace_init": ([ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                            ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
+    "rdn_check_blob": ([ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t], ctypes.c_int),
     "rdn_forward": ([ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                      ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
     "rdn_generate": ([ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, ctypes.POINTER(GenParams), ctypes.c_void_p,
                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "rdn_metrics": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                      ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "rdn_metrics_ex": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "rdn_acc_value": ([ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
 }
 
 EXPORTED = tuple(_SIGNATURES)

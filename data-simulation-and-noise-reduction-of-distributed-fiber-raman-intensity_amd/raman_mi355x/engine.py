@@ -13,16 +13,19 @@ from . import _lib
 ARCHS = ("DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN")
 ARCH_ID = {a: i for i, a in enumerate(ARCHS)}
 CBAM_ARCHS = ("ADSDN", "APIDN")
+CBAM_IDS = tuple(ARCH_ID[a] for a in CBAM_ARCHS)
 # Engine arithmetic modes (include/raman_mi355x.h rdn_dtype).  Every name here except
 # "bf16-unsafe" meets its north-star tolerance on every golden fixture (fp32: 1e-5 max-relative;
 # 16-bit modes: 2e-2 max-abs).  Single-rounding bf16 does NOT (0.24 on trained RRCDNet),
 # so it is reachable only under that explicit name; plain "bf16" / torch.bfloat16 is refused with a
 # pointer to the tolerance-meeting 16-bit modes instead of silently returning out-of-contract results.
-DTYPE_ID = {"fp32": 0, "float32": 0, "bf16-unsafe": 1, "bf16_unsafe": 1, "bf16x3": 2, "f16f8": 3, "f16": 4,
-            "float16": 4, "f16-plain": 4, "f16mix": 5}
-DTYPE_NAME = {0: "fp32", 1: "bf16-unsafe", 2: "bf16x3", 3: "f16f8", 4: "f16", 5: "f16mix"}
+DTYPE_ID = {"fp32": 0, "float32": 0, "bf16-unsafe": 1, "bf16_unsafe": 1, "bf16x3": 2, "f16f8": 3, "f16-plain": 4,
+            "f16mix": 5}
+DTYPE_NAME = {0: "fp32", 1: "bf16-unsafe", 2: "bf16x3", 3: "f16f8", 4: "f16-plain", 5: "f16mix"}
 SAFE_16BIT = ("f16", "f16f8", "bf16x3")
 F16, F16MIX = 4, 5
+# every spelling of "f16" means one thing: the fastest arithmetic within the 2e-2 bar for the network
+_F16_SPELLINGS = ("f16", "float16", "half")
 
 
 def default_correction_mask(arch):
@@ -35,19 +38,42 @@ def default_correction_mask(arch):
 def correction_mask(arch, dtype, host_blob):
     """Correction mask recorded in a packed (host) blob."""
     m = ctypes.c_uint64()
-    _lib.check(_lib.lib().rdn_get_correction_mask(_arch(arch), _dtype(dtype), ctypes.c_void_p(host_blob.data_ptr()),
-                                                  host_blob.numel(), ctypes.byref(m)), "rdn_get_correction_mask")
+    _lib.check(_lib.lib().rdn_get_correction_mask(_arch(arch), resolve_dtype(arch, dtype),
+                                                  ctypes.c_void_p(host_blob.data_ptr()), host_blob.numel(),
+                                                  ctypes.byref(m)), "rdn_get_correction_mask")
     return m.value
 
 
+def check_blob(arch, dtype, host_blob):
+    """Raise unless ``host_blob`` (a CPU uint8 tensor) was packed by rdn_pack for (arch, dtype)."""
+    _lib.check(_lib.lib().rdn_check_blob(_arch(arch), resolve_dtype(arch, dtype), ctypes.c_void_p(host_blob.data_ptr()),
+                                         host_blob.numel()), "rdn_check_blob")
+
+
 def resolve_dtype(arch, dtype):
-    """ABI dtype code for a user dtype.  'f16' is the fastest arithmetic within the 2e-2 bar: plain f16
-    (RDN_F16) where that suffices, f16 with the compiled-in e4m3-corrected layers (RDN_F16MIX) where it
-    does not (RRCDNet).  'f16-plain' forces RDN_F16 everywhere."""
-    code = _dtype(dtype)
-    if dtype == "f16" and default_correction_mask(arch):
-        code = F16MIX
-    return code
+    """ABI dtype code (rdn_dtype) for a user dtype.  'f16' (also 'float16' and torch.float16) is the
+    fastest arithmetic within the 2e-2 bar: plain f16 (RDN_F16) where that suffices, f16 with the
+    compiled-in e4m3-corrected layers (RDN_F16MIX) where it does not (RRCDNet).  'f16-plain' forces
+    RDN_F16 everywhere, 'f16mix' RDN_F16MIX.  An integer is taken as an ABI code unchanged."""
+    if isinstance(dtype, int) and not isinstance(dtype, bool):
+        if dtype not in DTYPE_NAME:
+            raise ValueError(f"unknown engine dtype code {dtype}")
+        return dtype
+    if isinstance(dtype, torch.dtype):
+        dtype = {torch.float32: "fp32", torch.bfloat16: "bf16", torch.float16: "f16"}.get(dtype, str(dtype))
+    if dtype in _F16_SPELLINGS:
+        return F16MIX if default_correction_mask(arch) else F16
+    return _dtype(dtype)
+
+
+def dtype_name(dtype, arch=None):
+    """User-level name of a dtype: 'f16' for every f16 spelling (the network's fastest mode within
+    2e-2), else the name of its ABI code ('f16-plain' = RDN_F16, 'f16mix' = RDN_F16MIX)."""
+    if isinstance(dtype, torch.dtype) and dtype == torch.float16:
+        return "f16"
+    if isinstance(dtype, str) and dtype in _F16_SPELLINGS:
+        return "f16"
+    return DTYPE_NAME[resolve_dtype(arch, dtype) if arch is not None else _dtype(dtype)]
 
 
 def _arch(arch):
@@ -60,19 +86,22 @@ def _arch(arch):
 
 
 def _dtype(dtype):
+    """Code of an arch-independent dtype name ('f16' depends on the network: resolve_dtype)."""
     if isinstance(dtype, int) and dtype in DTYPE_NAME:
         return dtype
     if isinstance(dtype, torch.dtype):
         dtype = {torch.float32: "fp32", torch.bfloat16: "bf16", torch.float16: "f16"}.get(dtype, str(dtype))
+    if dtype in _F16_SPELLINGS:
+        raise ValueError("engine dtype 'f16' resolves per network: use resolve_dtype(arch, 'f16')")
     if dtype in ("bf16", "bfloat16"):
         raise ValueError("engine dtype 'bf16' (one bf16 rounding per operand) does not meet the 2e-2 bf16 "
                          "tolerance on trained weights (0.24 on trained RRCDNet); use 'f16', 'f16f8' or 'bf16x3' "
                          f"({', '.join(SAFE_16BIT)}: within 2e-2), or opt in explicitly with 'bf16-unsafe'")
     try:
         return DTYPE_ID[dtype]
-    except KeyError:
-        raise ValueError(f"unknown engine dtype {dtype!r}; expected one of 'fp32', 'f16', 'f16f8', 'bf16x3', "
-                         "'bf16-unsafe'") from None
+    except (KeyError, TypeError):
+        raise ValueError(f"unknown engine dtype {dtype!r}; expected one of 'fp32', 'f16', 'f16-plain', 'f16f8', "
+                         "'bf16x3', 'bf16-unsafe'") from None
 
 
 def _stream(device):
@@ -91,7 +120,7 @@ def param_names(arch):
 
 def packed_size(arch, dtype):
     n = ctypes.c_size_t()
-    _lib.check(_lib.lib().rdn_packed_size(_arch(arch), _dtype(dtype), ctypes.byref(n)), "rdn_packed_size")
+    _lib.check(_lib.lib().rdn_packed_size(_arch(arch), resolve_dtype(arch, dtype), ctypes.byref(n)), "rdn_packed_size")
     return n.value
 
 
@@ -104,9 +133,10 @@ def pack(arch, state_dict, dtype, device):
     host = [state_dict[k].detach().to("cpu", torch.float32).contiguous() for k in names]
     ptrs = (ctypes.c_void_p * len(host))(*[t.data_ptr() for t in host])
     numels = (ctypes.c_int64 * len(host))(*[t.numel() for t in host])
-    size = packed_size(arch, dtype)
+    code = resolve_dtype(arch, dtype)
+    size = packed_size(arch, code)
     blob = torch.empty(size, dtype=torch.uint8)
-    _lib.check(_lib.lib().rdn_pack(_arch(arch), _dtype(dtype), ptrs, numels, len(host),
+    _lib.check(_lib.lib().rdn_pack(_arch(arch), code, ptrs, numels, len(host),
                                    ctypes.c_void_p(blob.data_ptr()), size), "rdn_pack")
     return blob.to(device)
 
@@ -133,13 +163,56 @@ def _check_out(t, name, shape, device, dtype=torch.float32):
         raise ValueError(f"{name} must be contiguous")
 
 
-def forward(arch, dtype, packed, x, out=None, check=True):
+class Workspace:
+    """Device scratch of the CBAM team kernels for (arch, dtype, L) on one device and stream, reused
+    across forwards.  Its hand-off error word is sticky: ``check()`` waits for the stream once and
+    raises EngineError if any forward since the last check timed out (rdn_forward_status), so a
+    batched driver checks once at the end instead of host-syncing every batch."""
+
+    def __init__(self, arch, dtype, n, L, device, stream=None):
+        self.arch, self.code, self.L = _arch(arch), resolve_dtype(arch, dtype), int(L)
+        self.device = torch.device(device)
+        self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self.n = int(n)
+        sz = ctypes.c_size_t()
+        lib_ = _lib.lib()
+        sp = ctypes.c_void_p(self.stream.cuda_stream)
+        _lib.check(lib_.rdn_workspace_size(self.arch, self.code, self.n, self.L, ctypes.byref(sz), sp),
+                   "rdn_workspace_size")
+        self.bytes = sz.value
+        self.buf = torch.empty(self.bytes, dtype=torch.uint8, device=self.device) if self.bytes else None
+        _lib.check(lib_.rdn_workspace_init(self.arch, self.code, self.n, self.L, self.ptr, self.bytes, sp),
+                   "rdn_workspace_init")
+
+    @property
+    def ptr(self):
+        return ctypes.c_void_p(self.buf.data_ptr() if self.buf is not None else 0)
+
+    def fits(self, arch, code, n, L, device):
+        return (self.arch, self.code, self.L, self.device) == (_arch(arch), code, int(L), torch.device(device)) \
+            and (self.n >= n or self.bytes_for(n) <= self.bytes)
+
+    def bytes_for(self, n):
+        sz = ctypes.c_size_t()
+        _lib.check(_lib.lib().rdn_workspace_size(self.arch, self.code, int(n), self.L, ctypes.byref(sz),
+                                                 ctypes.c_void_p(self.stream.cuda_stream)), "rdn_workspace_size")
+        return sz.value
+
+    def check(self):
+        """Wait for the stream; raise if a CBAM hand-off of any forward since the last check timed out."""
+        _lib.check(_lib.lib().rdn_forward_status(self.arch, self.code, self.n, self.L, self.ptr, self.bytes,
+                                                 ctypes.c_void_p(self.stream.cuda_stream)), "rdn_forward_status")
+
+
+def forward(arch, dtype, packed, x, out=None, check=True, workspace=None):
     """y = Model(x) for x float32 (N, 1, L) (or (N, L)) on the GPU.
 
-    The CBAM networks run one team-persistent kernel whose workgroups hand off statistics; with
-    ``check`` (default) the call waits for it and raises EngineError if a hand-off timed out
-    (rdn_forward_status).  ``check=False`` keeps the launch asynchronous (benchmarks), and the
-    affected outputs are NaN in that case."""
+    ``dtype`` is an engine dtype name or ABI code (resolve_dtype).  The CBAM networks run one
+    team-persistent kernel whose workgroups hand off statistics.  With ``check`` (default) the call
+    waits for it and raises EngineError if a hand-off timed out (rdn_forward_status).  A batched
+    caller passes one ``Workspace`` to every forward with ``check=False`` and calls
+    ``workspace.check()`` once at the end (the error word is sticky); ``check=False`` without a
+    workspace keeps the launch asynchronous and unchecked (benchmarks: the affected outputs are NaN)."""
     _check_cuda_f32(x, "input")
     if x.dim() == 3 and x.shape[1] != 1:
         raise ValueError(f"expected (N, 1, L) input, got {tuple(x.shape)}")
@@ -147,23 +220,24 @@ def forward(arch, dtype, packed, x, out=None, check=True):
         raise ValueError(f"expected (N, 1, L) input, got {tuple(x.shape)}")
     x = x.contiguous()
     n, L = x.shape[0], x.shape[-1]
+    a, code = _arch(arch), resolve_dtype(arch, dtype)
     y = torch.empty_like(x) if out is None else out
     if out is not None:
         _check_out(y, "out", x.shape, x.device)
     if y.data_ptr() < x.data_ptr() + x.numel() * 4 and x.data_ptr() < y.data_ptr() + y.numel() * 4:
         raise ValueError("out must not overlap the input (tiles re-read input halos while outputs are written)")
-    ws_bytes = ctypes.c_size_t()
+    ws = workspace
+    if ws is None and a in CBAM_IDS:
+        ws = Workspace(a, code, n, L, x.device)
+    elif ws is not None and not ws.fits(a, code, n, L, x.device):
+        raise ValueError("workspace was made for another network, dtype, length, device or a smaller batch")
     L_ = _lib.lib()
-    _lib.check(L_.rdn_workspace_size(_arch(arch), _dtype(dtype), n, L, ctypes.byref(ws_bytes)), "rdn_workspace_size")
-    ws = torch.empty(ws_bytes.value, dtype=torch.uint8, device=x.device) if ws_bytes.value else None
-    _lib.check(L_.rdn_forward(_arch(arch), _dtype(dtype), ctypes.c_void_p(packed.data_ptr()),
-                              ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), n, L,
-                              ctypes.c_void_p(ws.data_ptr() if ws is not None else 0), ws_bytes.value,
+    _lib.check(L_.rdn_forward(a, code, ctypes.c_void_p(packed.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                              ctypes.c_void_p(y.data_ptr()), n, L,
+                              ws.ptr if ws is not None else ctypes.c_void_p(0), ws.bytes if ws is not None else 0,
                               _stream(x.device)), "rdn_forward")
-    if check and _arch(arch) in (ARCH_ID[a] for a in CBAM_ARCHS):
-        _lib.check(L_.rdn_forward_status(_arch(arch), _dtype(dtype), n, L,
-                                         ctypes.c_void_p(ws.data_ptr() if ws is not None else 0), ws_bytes.value,
-                                         _stream(x.device)), "rdn_forward_status")
+    if check and ws is not None:
+        ws.check()
     return y
 
 
@@ -195,10 +269,17 @@ def generate(n, seed, first_index=0, signal_length=10000, snr_range=(20.0, 37.0)
     return clean, noisy, snr, nstd
 
 
-def metrics(y, clean, sums=None, per_spectrum=True):
-    """Per-spectrum [MSE, SSIM, Smoothness, Peak2Peak] (fp64, (n, 4)) and accumulated sums (fp64 [5])."""
+def metrics(y, clean, sums=None, per_spectrum=True, acc=None):
+    """Per-spectrum [MSE, SSIM, Smoothness, Peak2Peak] (fp64, (n, 4)) and accumulated fp64 sums [5].
+
+    ``clean`` may be float32 (the device simulator) or float64 (a test.npz as evaulate.py:61-62 loads
+    it; the metrics then see the same float64 clean values as evaulate.py:34-35).  ``acc``: an
+    exact accumulator (new_acc) that this batch is added to (rdn_metrics_ex)."""
     _check_cuda_f32(y, "denoised")
-    _check_cuda_f32(clean, "clean")
+    if not (torch.is_tensor(clean) and clean.is_cuda):
+        raise RuntimeError("raman_mi355x runs on the GPU only: clean must be a CUDA (HIP) tensor")
+    if clean.dtype not in (torch.float32, torch.float64):
+        raise TypeError(f"clean must be float32 or float64, got {clean.dtype}")
     y = y.reshape(y.shape[0], -1).contiguous()
     clean = clean.reshape(clean.shape[0], -1).contiguous()
     if y.shape != clean.shape:
@@ -211,7 +292,29 @@ def metrics(y, clean, sums=None, per_spectrum=True):
         sums = torch.zeros(5, dtype=torch.float64, device=y.device)
     else:
         _check_out(sums, "sums", (5,), y.device, torch.float64)   # fp64 atomics into sums[0..4]
-    _lib.check(_lib.lib().rdn_metrics(ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(clean.data_ptr()), n, L,
-                                      ctypes.c_void_p(per.data_ptr() if per is not None else 0),
-                                      ctypes.c_void_p(sums.data_ptr()), _stream(y.device)), "rdn_metrics")
+    if acc is not None:
+        _check_out(acc, "acc", (_lib.ACC_WORDS,), y.device, torch.int64)
+    _lib.check(_lib.lib().rdn_metrics_ex(ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(clean.data_ptr()),
+                                         int(clean.dtype == torch.float64), n, L,
+                                         ctypes.c_void_p(per.data_ptr() if per is not None else 0),
+                                         ctypes.c_void_p(sums.data_ptr()),
+                                         ctypes.c_void_p(acc.data_ptr() if acc is not None else 0),
+                                         _stream(y.device)), "rdn_metrics_ex")
     return per, sums
+
+
+def new_acc(device):
+    """A zeroed exact metric accumulator (RDN_ACC_WORDS int64) on ``device``."""
+    return torch.zeros(_lib.ACC_WORDS, dtype=torch.int64, device=device)
+
+
+def acc_value(acc):
+    """{ΣMSE, ΣSSIM, ΣSmoothness, ΣPeak2Peak, count} (float64 [5], CPU) of an exact accumulator: each
+    sum is the exact total rounded once (rdn_acc_value)."""
+    h = acc.detach().to("cpu", torch.int64).contiguous()
+    if h.numel() != _lib.ACC_WORDS:
+        raise ValueError(f"accumulator must have {_lib.ACC_WORDS} words")
+    out = torch.empty(5, dtype=torch.float64)
+    _lib.check(_lib.lib().rdn_acc_value(ctypes.cast(h.data_ptr(), ctypes.POINTER(ctypes.c_int64)),
+                                        ctypes.cast(out.data_ptr(), ctypes.POINTER(ctypes.c_double))), "rdn_acc_value")
+    return out

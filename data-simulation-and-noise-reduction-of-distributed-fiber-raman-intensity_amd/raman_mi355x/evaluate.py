@@ -1,19 +1,33 @@
-"""Batched, on-device replacement of the reference evaluation harness (*/evaulate.py).
+"""Batched, on-device replacements of the reference evaluation harness (*/evaulate.py).
 
 ``evaluate(model, noisy_data, clean_data)`` returns the same dict as evaulate.py:25-39
 ({MSE, SSIM, Smoothness, Peak2Peak} averaged over spectra) but runs the forward in batches and the
-metrics in the fp64 device kernel instead of a batch-1 loop with a host sync per spectrum.  Under
-torch.distributed each rank evaluates its contiguous shard and the metric sums are all-reduced.
-``write_metrics`` produces evaulate.py:78-80's ``metrics.txt`` format.
+metrics in the fp64 device kernel instead of a batch-1 loop with a host sync per spectrum.  The
+clean reference stays float64 (evaulate.py:34-35 compares against the float64 test.npz arrays).
+
+``evaluate_synthetic(models, total, ...)`` is the config-4 driver: a fixed total of
+N simulator spectra, rank r of W owning indices [r·N/W, (r+1)·N/W), chunked generate -> forward ->
+metric sums per network, one all-reduce at the end.  The simulator is counter-based and the sums
+are exact integer accumulators (rdn_metrics_ex), so the four means are the same bits for any W,
+batch size or atomics order.
+
+Under torch.distributed each rank evaluates its contiguous shard and the metric accumulators are
+all-reduced (RCCL over xGMI for CUDA tensors).  The CBAM networks' hand-off status is checked once
+per network at the end (engine.Workspace), not per batch.  ``write_metrics`` produces
+evaulate.py:78-80's ``metrics.txt`` format.
 """
 import os
+import time
 from datetime import datetime
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from . import engine
-from .distributed import all_reduce_sums, means, shard
+from .distributed import shard, world
+
+KEYS = ("MSE", "SSIM", "Smoothness", "Peak2Peak")
 
 
 def _as_rows(a):
@@ -21,6 +35,38 @@ def _as_rows(a):
         return a.reshape(a.shape[0], -1)
     a = np.asarray(a)
     return a.reshape(a.shape[0], -1)
+
+
+def _all_reduce_acc(acc):
+    """SUM all-reduce of an exact accumulator (int64, exact under any reduction order)."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if dist.get_backend() == "gloo" and acc.is_cuda:        # gloo reduces host tensors
+            h = acc.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM)
+            acc.copy_(h)
+        else:
+            dist.all_reduce(acc, op=dist.ReduceOp.SUM)
+    return acc
+
+
+def means_from_acc(acc):
+    """{MSE, SSIM, Smoothness, Peak2Peak} means of an exact accumulator (evaulate.py:39)."""
+    s = engine.acc_value(acc).tolist()
+    if s[4] <= 0:
+        raise ValueError("no spectra were evaluated")
+    return {k: s[i] / s[4] for i, k in enumerate(KEYS)}
+
+
+def _model_forward(model, x, ws):
+    """The module's forward without the per-call hand-off check (one Workspace.check at the end)."""
+    return engine.forward(model.ARCH, model.engine_code, model.packed_weights(x.device), x, check=False,
+                          workspace=ws)
+
+
+def _workspace(model, n, L, device):
+    if model.ARCH not in engine.CBAM_ARCHS:
+        return None
+    return engine.Workspace(model.ARCH, model.engine_code, n, L, device)
 
 
 def evaluate(model, noisy_data, clean_data, batch_size=1024, device=None):
@@ -33,16 +79,75 @@ def evaluate(model, noisy_data, clean_data, batch_size=1024, device=None):
     if noisy.shape != clean.shape:
         raise ValueError(f"noisy {tuple(noisy.shape)} vs clean {tuple(clean.shape)}")
     lo, hi = shard(noisy.shape[0])
-    sums = torch.zeros(5, dtype=torch.float64, device=device)
+    L = noisy.shape[1]
+    acc = engine.new_acc(device)
+    ws = _workspace(model, min(batch_size, max(hi - lo, 1)), L, device)
+    # fp64 clean stays fp64 (the metrics compare against the same float64 values as evaulate.py)
+    cdt = torch.float64 if (clean.dtype == torch.float64 if torch.is_tensor(clean) else clean.dtype == np.float64) \
+        else torch.float32
     with torch.no_grad():
         for b0 in range(lo, hi, batch_size):
             b1 = min(hi, b0 + batch_size)
             x = torch.as_tensor(noisy[b0:b1], dtype=torch.float32).to(device).unsqueeze(1)
-            c = torch.as_tensor(clean[b0:b1], dtype=torch.float32).to(device)
-            y = model(x)
-            engine.metrics(y.squeeze(1), c, sums=sums, per_spectrum=False)
-    all_reduce_sums(sums)
-    return means(sums)
+            c = torch.as_tensor(clean[b0:b1], dtype=cdt).to(device)
+            y = _model_forward(model, x, ws)
+            engine.metrics(y.squeeze(1), c, per_spectrum=False, acc=acc)
+    if ws is not None:
+        ws.check()
+    _all_reduce_acc(acc)
+    return means_from_acc(acc)
+
+
+def evaluate_synthetic(models, total, seed=20250410, signal_length=10000, batch_size=8192, device=None,
+                       first_index=0, gen_kwargs=None, sync_timing=True):
+    """Config 4: ``total`` simulator spectra [first_index, first_index + total),
+    sharded over the ranks as [r·N/W, (r+1)·N/W), each chunk generated on the device, denoised by
+    every model in ``models`` (name -> module) and metered into that model's exact accumulator.
+    Returns {name: {"means", "spectra", "seconds", "spectra_per_s"}} with the all-reduced means
+    (identical for any world size) and the max-over-ranks wall time of the loop."""
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    device = torch.device(device)
+    gen_kwargs = gen_kwargs or {}
+    rank, W = world()
+    lo, hi = shard(total, rank, W)
+    L = int(signal_length)
+    B = max(1, min(batch_size, hi - lo)) if hi > lo else 1
+    clean = torch.empty((B, L), dtype=torch.float32, device=device)
+    noisy = torch.empty((B, L), dtype=torch.float32, device=device)
+    y = torch.empty((B, 1, L), dtype=torch.float32, device=device)
+    out = {}
+    with torch.no_grad():
+        for name, model in models.items():
+            model.eval()
+            acc = engine.new_acc(device)
+            ws = _workspace(model, B, L, device)
+            packed = model.packed_weights(device)
+            if dist.is_available() and dist.is_initialized():
+                dist.barrier()
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            for b0 in range(lo, hi, B):
+                nb = min(B, hi - b0)
+                engine.generate(nb, seed, first_index=first_index + b0, signal_length=L, device=device,
+                                out=(clean[:nb], noisy[:nb]), **gen_kwargs)
+                engine.forward(model.ARCH, model.engine_code, packed, noisy[:nb].view(nb, 1, L), out=y[:nb],
+                               check=False, workspace=ws)
+                engine.metrics(y[:nb].view(nb, L), clean[:nb], per_spectrum=False, acc=acc)
+            if ws is not None:
+                ws.check()                  # waits for the stream; raises on a timed-out hand-off
+            torch.cuda.synchronize(device)
+            el = time.perf_counter() - t0
+            t = torch.tensor([el], dtype=torch.float64)
+            if dist.is_available() and dist.is_initialized() and W > 1:
+                tt = t.to(device) if dist.get_backend() != "gloo" else t
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                t = tt.cpu()
+            _all_reduce_acc(acc)
+            el = float(t.item())
+            out[name] = {"means": means_from_acc(acc), "acc": acc.cpu().tolist(), "spectra": int(total),
+                         "seconds": el, "spectra_per_s": total / el if el > 0 else None}
+    return out
 
 
 def write_metrics(metrics, root="eval_results"):

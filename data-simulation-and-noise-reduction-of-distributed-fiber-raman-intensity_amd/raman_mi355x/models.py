@@ -83,7 +83,7 @@ class _EngineNet(nn.Module):
         'bf16-unsafe' one bf16 rounding per operand: fastest, NO tolerance guarantee (0.24 on trained
                       RRCDNet).  Plain 'bf16' is refused (engine._dtype)."""
         code = engine.resolve_dtype(self.ARCH, dtype)
-        self._engine_dtype = dtype if isinstance(dtype, str) and dtype in engine.DTYPE_ID else engine.DTYPE_NAME[code]
+        self._engine_dtype = engine.dtype_name(dtype, self.ARCH)
         self._engine_code = code
         return self
 

@@ -19,7 +19,7 @@
  *   rdn_generate
  *       -> generate_signals(num_samples, signal_length, snr_range, extreme_noise_prob, max_repeat)
  *                                                                  数据集产生.py:5-64
- *   rdn_metrics
+ *   rdn_metrics / rdn_metrics_ex / rdn_acc_value
  *       -> compute_mse / compute_smoothness / compute_peak_to_peak + skimage SSIM, averaged
  *                                                                  <model>/evaulate.py:14-39
  */
@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RDN_ABI_VERSION 2
+#define RDN_ABI_VERSION 3
 
 typedef enum {
   RDN_DENOISECNN = 0, /* 1DCNN/train.py   class DenoiseCNN */
@@ -105,6 +105,14 @@ int rdn_packed_size(int arch, int dtype, size_t* bytes);
 int rdn_pack(int arch, int dtype, const float* const* tensors, const int64_t* numels, int n_tensors,
              void* dst, size_t cap);
 
+/* Blob layout tag: rdn_pack writes RDN_BLOB_MAGIC | arch << 8 | dtype into a word of the small
+ * section, and rdn_check_blob verifies that a host blob was packed for (arch, dtype) and is at
+ * least rdn_packed_size bytes.  The blob layouts differ per dtype (e.g. an RDN_F16MIX blob holds one
+ * more record than an RDN_F16F8 one): rdn_forward needs a blob packed for the same (arch, dtype).
+ * The RDN_F16MIX kernels also check the tag on the device and write NaN outputs on a mismatch. */
+#define RDN_BLOB_MAGIC 0x52440000u
+int rdn_check_blob(int arch, int dtype, const void* host_blob, size_t bytes);
+
 /* Per-layer correction mask (bit i = big layer i, execution order of rdn_param_names' convs, runs
  * the e4m3 correction).  default: the RDN_F16MIX pattern of `arch` (0 = plain RDN_F16 already meets
  * 2e-2 there, and RDN_F16MIX is not built); get: read back from a packed RDN_F16F8 (all ones) or
@@ -112,8 +120,15 @@ int rdn_pack(int arch, int dtype, const float* const* tensors, const int64_t* nu
 int rdn_default_correction_mask(int arch, uint64_t* mask);
 int rdn_get_correction_mask(int arch, int dtype, const void* host_blob, size_t bytes, uint64_t* mask);
 
-/* Device scratch rdn_forward needs for a batch (0 for the fully fused networks). */
-int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes);
+/* Device scratch rdn_forward needs for a batch on the device of `stream` (0 for the fully fused
+ * networks; the CBAM team geometry depends on the device's CU count and occupancy). */
+int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes, void* stream);
+
+/* Prepare a newly allocated workspace for rdn_forward on `stream`: clears its hand-off error word
+ * (the word is sticky across forwards until rdn_forward_status reads and clears it, so one status
+ * call after many forwards that share a workspace covers all of them). */
+int rdn_workspace_init(int arch, int dtype, int64_t n, int64_t L, void* workspace, size_t workspace_bytes,
+                       void* stream);
 
 /* y[n][L] = Model(x[n][L]) on the device.  x, y: fp32 device pointers (the (N,1,L) tensor is
  * (N,L) contiguous) that must not overlap (RDN_EINVAL: tiles re-read input halos while outputs are
@@ -121,12 +136,14 @@ int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes)
 int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* y, int64_t n, int64_t L,
                 void* workspace, size_t workspace_bytes, void* stream);
 
-/* Completion status of the rdn_forward last enqueued on `stream` with these arguments and this
- * workspace: waits for the stream (hipStreamSynchronize), then, for the CBAM networks (ADSDN,
- * APIDN), reads the team kernel's hand-off error word from the workspace.  RDN_EHIP if a team wait
- * timed out (co-residency broken by a concurrent kernel; the affected spectra's outputs are NaN) or
- * the stream reported an error; RDN_OK otherwise.  Replaces nothing in the reference (its forward
- * is synchronous PyTorch); the Python module calls it after every CBAM forward. */
+/* Completion status of every rdn_forward enqueued on `stream` with this workspace since the last
+ * status call (or rdn_workspace_init): waits for the stream (hipStreamSynchronize), then, for the
+ * CBAM networks (ADSDN, APIDN), reads and clears the team kernel's sticky hand-off error word.
+ * RDN_EHIP if a team wait timed out (co-residency broken by a concurrent kernel; the affected
+ * spectra's outputs are NaN) or the stream reported an error; RDN_ESIZE if the workspace is smaller
+ * than this device's team geometry needs; RDN_OK otherwise.  Replaces nothing in the reference (its
+ * forward is synchronous PyTorch): the Python module calls it after each CBAM forward of the
+ * evaulate.py loop, the batched evaluate drivers once at the end. */
 int rdn_forward_status(int arch, int dtype, int64_t n, int64_t L, void* workspace, size_t workspace_bytes,
                        void* stream);
 
@@ -151,6 +168,30 @@ int rdn_generate(uint64_t seed, uint64_t first_index, int64_t n, const rdn_gen_p
  * L must be >= 7 (SSIM window). */
 int rdn_metrics(const float* y, const float* clean, int64_t n, int64_t L, double* per_spectrum,
                 double* sums, void* stream);
+
+/* Exact metric accumulator: RDN_ACC_WORDS int64 on the device.  Metric k (MSE, SSIM, Smoothness,
+ * Peak2Peak) owns words [k * RDN_ACC_STRIDE, ...): RDN_ACC_LIMBS limbs, limb j holding the sum of the
+ * spectra's 32-bit chunks of weight 2^(32 j - RDN_ACC_FRAC_BITS) (values truncated toward zero below
+ * 2^-128), then a count of values that were non-finite or >= 2^64 in magnitude; word RDN_ACC_COUNT
+ * counts spectra.  Integer addition is associative, so the accumulated bits do not depend on the
+ * batch split, the atomics' order or the number of ranks whose accumulators are summed (all-reduce
+ * SUM over int64), for up to 2^31 spectra per accumulator. */
+#define RDN_ACC_LIMBS 6
+#define RDN_ACC_FRAC_BITS 128
+#define RDN_ACC_STRIDE (RDN_ACC_LIMBS + 1)
+#define RDN_ACC_COUNT (4 * RDN_ACC_STRIDE)
+#define RDN_ACC_WORDS (RDN_ACC_COUNT + 1)
+
+/* rdn_metrics with the clean reference in fp32 (clean_is_f64 = 0) or fp64 (1, e.g. a test.npz as
+ * the reference loads it), and an optional exact accumulator `acc` (device, RDN_ACC_WORDS int64,
+ * ACCUMULATED).  per_spectrum, sums and acc may each be NULL. */
+int rdn_metrics_ex(const float* y, const void* clean, int clean_is_f64, int64_t n, int64_t L, double* per_spectrum,
+                   double* sums, int64_t* acc, void* stream);
+
+/* Host: {ΣMSE, ΣSSIM, ΣSmoothness, ΣPeak2Peak, count} from a HOST copy of an exact accumulator, each
+ * sum the exact accumulated value rounded once to the nearest double (NaN for a metric with an
+ * out-of-range value). */
+int rdn_acc_value(const int64_t* acc, double* sums);
 
 #ifdef __cplusplus
 }

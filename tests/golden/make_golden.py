@@ -177,8 +177,93 @@ def metric_goldens(clean, den):
         return np.load(os.path.join(td, "out.npy"))
 
 
+HELDOUT_SEED_DATA = 20261017        # inputs no fixture or tuning run has seen
+HELDOUT_STEPS = 2500
+
+
+def train_heldout(cls, gen, steps=HELDOUT_STEPS, L=1000, batch=16, lr=3e-4):
+    """A longer CPU Adam run at the reference's own LR (RRCDNet/train.py:118) on a training pool drawn
+    with another seed than every other fixture: the held-out weight set for the RDN_F16MIX
+    correction mask (tools/f16mix_select.py chose that mask on the model_RRCDNet.npz fixtures)."""
+    torch.manual_seed(101)
+    np.random.seed(4242)
+    clean, noisy, _, _ = gen(512, signal_length=L)
+    xc = torch.tensor(clean, dtype=torch.float32).unsqueeze(1)
+    xn = torch.tensor(noisy, dtype=torch.float32).unsqueeze(1)
+    model = cls()
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    g = torch.Generator().manual_seed(101)
+    model.train()
+    t0 = time.time()
+    losses = []
+    for step in range(steps):
+        idx = torch.randint(0, xn.shape[0], (batch,), generator=g)
+        opt.zero_grad()
+        loss = torch.nn.functional.mse_loss(model(xn[idx]), xc[idx])
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+        if step % 250 == 0:
+            print(f"  step {step}: loss {np.mean(losses[-50:]):.6f} ({time.time() - t0:.0f}s)", flush=True)
+    print(f"  trained {cls.__name__}: {steps} steps, final loss {np.mean(losses[-100:]):.6f}, {time.time()-t0:.1f}s")
+    model.eval()
+    return {k: v.detach().clone() for k, v in model.state_dict().items()}, float(np.mean(losses[-100:]))
+
+
+def make_heldout(arch="RRCDNet"):
+    """heldout_<arch>.npz: held-out trained weights + fresh reference-generator inputs (half of them
+    spiked: extreme_noise_prob = 1) + the reference's fp32 and float64 outputs on them."""
+    gen = _refload.load_generate_signals()
+    cls = _refload.load_model_class(arch)
+    sd, loss = train_heldout(cls, gen)
+    np.random.seed(HELDOUT_SEED_DATA)
+    c1, n1, _, _ = gen(4, signal_length=10000)
+    c2, n2, _, _ = gen(4, signal_length=10000, extreme_noise_prob=1.0)
+    c3, n3, _, _ = gen(2, signal_length=2333, extreme_noise_prob=1.0)
+    rec = {f"w::{k}": v.numpy() for k, v in sd.items()}
+    rec["train_steps"] = np.array(HELDOUT_STEPS)
+    rec["train_loss"] = np.array(loss)
+    sets = {"main": np.concatenate([n1, n2]).astype(np.float32), "odd": n3.astype(np.float32)}
+    for name, x in sets.items():
+        rec[f"in_{name}"] = x
+    rec["clean_main"] = np.concatenate([c1, c2])
+    rec["clean_odd"] = c3
+    for name, y in ref_outputs(cls, sd, sets).items():
+        rec[f"ref_{name}"] = y
+    for name, y in ref_outputs(cls, sd, sets, double=True).items():
+        rec[f"f64_{name}"] = y
+    np.savez_compressed(os.path.join(HERE, f"heldout_{arch}.npz"), **rec)
+    print(f"heldout_{arch}.npz written: out range [{rec['ref_main'].min():.3f}, {rec['ref_main'].max():.3f}]")
+
+
+def spike_stats_reference():
+    """generator_stats.json["spikes"]: spike count / width / start / amplitude / sign histograms of
+    1000 spectra drawn by the reference generator with every spectrum spiked
+    (extreme_noise_prob = 1), recovered by tests/spike_stats.py (the GPU test applies the same
+    recovery to the device simulator's spectra)."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import spike_stats
+    gen = _refload.load_generate_signals()
+    np.random.seed(SEED_DATA + 1)
+    clean, noisy, _, nstd = gen(1000, extreme_noise_prob=1.0)
+    rec = spike_stats.collect(clean, noisy, nstd[:, 0])
+    path = os.path.join(HERE, "generator_stats.json")
+    with open(path) as fh:
+        stats = json.load(fh)
+    stats["spikes"] = rec
+    with open(path, "w") as fh:
+        json.dump(stats, fh)
+    print("spikes:", rec)
+
+
 def main():
     torch.set_num_threads(os.cpu_count())
+    if "--spikes" in sys.argv:
+        spike_stats_reference()
+        return
+    if "--heldout" in sys.argv:
+        make_heldout()
+        return
     gen = _refload.load_generate_signals()
     inp = make_inputs(gen)
     np.savez_compressed(os.path.join(HERE, "inputs.npz"), **inp)

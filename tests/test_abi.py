@@ -27,7 +27,7 @@ def test_exports_every_declared_symbol(lib):
     assert declared == set(_lib.EXPORTED), declared ^ set(_lib.EXPORTED)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.rdn_version() == 2
+    assert lib.rdn_version() == 3
 
 
 def test_library_built_from_these_sources(lib):
@@ -48,10 +48,101 @@ def test_plain_bf16_is_refused_and_unsafe_mode_is_explicit():
     assert engine._dtype("f16f8") == 3 and engine._dtype(torch.float32) == 0
 
 
+@pytest.mark.parametrize("spelling", ["f16", "float16", torch.float16])
+def test_every_f16_spelling_selects_the_same_arithmetic(spelling):
+    """'f16', 'float16' and torch.float16 all mean the network's fastest mode within 2e-2: RDN_F16MIX
+    on RRCDNet (plain f16 misses the bar there), RDN_F16 elsewhere; only 'f16-plain' opts out.  The
+    functional engine API resolves the same way as the module."""
+    import raman_mi355x as R
+    from raman_mi355x import engine
+    for arch in ARCHS:
+        code = engine.resolve_dtype(arch, spelling)
+        assert code == (5 if arch == "RRCDNet" else 4), (arch, code)
+        m = R.MODELS[arch]().set_engine_dtype(spelling)
+        assert m.engine_code == code and m.engine_dtype == "f16"
+        assert engine.resolve_dtype(arch, "f16-plain") == 4
+        assert R.MODELS[arch]().set_engine_dtype("f16-plain").engine_dtype == "f16-plain"
+    assert engine.packed_size("RRCDNet", spelling) == engine.packed_size("RRCDNet", "f16mix")
+    with pytest.raises(ValueError, match="resolves per network"):
+        engine._dtype(spelling)
+
+
+def test_f16mix_is_refused_for_other_networks_before_dispatch(lib):
+    """RDN_F16MIX exists for RRCDNet only: every entry point refuses it for the other networks with
+    RDN_EUNSUPPORTED before any per-network (e.g. CBAM) dispatch."""
+    n = ctypes.c_size_t()
+    for arch in (0, 2, 3, 4, 5):
+        assert lib.rdn_workspace_size(arch, 5, 4, 1000, ctypes.byref(n), None) == -2
+        assert b"RRCDNet" in lib.rdn_last_error()
+        assert lib.rdn_forward(arch, 5, ctypes.c_void_p(1 << 32), ctypes.c_void_p(1 << 33), ctypes.c_void_p(1 << 34),
+                               1, 1000, None, 0, None) == -2
+        assert lib.rdn_forward_status(arch, 5, 1, 1000, None, 0, None) == -2
+        assert lib.rdn_workspace_init(arch, 5, 1, 1000, None, 0, None) == -2
+
+
+def test_blob_layout_tag(lib):
+    """rdn_pack tags every blob with (arch, dtype); rdn_check_blob / rdn_get_correction_mask refuse a
+    blob of another layout (an RDN_F16F8 blob is one record short of what RDN_F16MIX reads)."""
+    from raman_mi355x import engine, _lib
+    sd = golden_state_dict("RRCDNet", "synth")
+    b8 = engine.pack("RRCDNet", sd, "f16f8", "cpu")
+    bm = engine.pack("RRCDNet", sd, "f16mix", "cpu")
+    engine.check_blob("RRCDNet", "f16f8", b8)
+    engine.check_blob("RRCDNet", "f16", bm)
+    assert engine.correction_mask("RRCDNet", "f16", bm) == 0x7 << 12
+    with pytest.raises(_lib.EngineError, match="needs"):
+        engine.check_blob("RRCDNet", "f16mix", b8)                 # too small for the F16MIX layout
+    padded = torch.cat([b8, torch.zeros(bm.numel() - b8.numel(), dtype=torch.uint8)])
+    with pytest.raises(_lib.EngineError, match="dtype 3, not arch 1 dtype 5"):
+        engine.check_blob("RRCDNet", "f16mix", padded)
+    with pytest.raises(_lib.EngineError, match="no layout tag"):
+        engine.check_blob("RRCDNet", "f16mix", torch.zeros_like(bm))
+    for arch in ARCHS:
+        for dt in ("fp32", "f16-plain", "f16f8"):
+            engine.check_blob(arch, dt, engine.pack(arch, golden_state_dict(arch, "synth"), dt, "cpu"))
+
+
+def _acc_of(values):
+    """Host restatement of the device accumulator (metrics.hip to_limbs): limbs of one metric."""
+    from fractions import Fraction
+    from raman_mi355x import _lib
+    limbs = [0] * _lib.ACC_LIMBS
+    for v in values:
+        f = Fraction(v) * 2 ** _lib.ACC_FRAC_BITS
+        mag = abs(f.numerator) // f.denominator                    # truncation toward zero
+        for j in range(_lib.ACC_LIMBS):
+            c = (mag >> (32 * j)) & 0xffffffff
+            limbs[j] += -c if v < 0 else c
+    return limbs
+
+
+def test_exact_accumulator_rounds_the_exact_sum_once(lib):
+    """rdn_acc_value: the exact total of the (2^-128-truncated) values, rounded once to double --
+    independent of summation order (the reason config-4 sums are identical for any world size)."""
+    from fractions import Fraction
+    from raman_mi355x import engine, _lib
+    rng = np.random.default_rng(5)
+    vals = [np.concatenate([rng.uniform(-1, 1, 500) * 10.0 ** rng.integers(-12, 12, 500),
+                            [1e-40, -3e-39, 2.0 ** 63, -(2.0 ** 62), 0.1, 0.2, 0.3]]) for _ in range(4)]
+    acc = torch.zeros(_lib.ACC_WORDS, dtype=torch.int64)
+    for k in range(4):
+        acc[k * _lib.ACC_STRIDE: k * _lib.ACC_STRIDE + _lib.ACC_LIMBS] = torch.tensor(_acc_of(vals[k]))
+    acc[_lib.ACC_COUNT] = 507
+    out = engine.acc_value(acc).numpy()
+    for k in range(4):
+        exact = sum(Fraction(abs(Fraction(v)) * 2 ** 128).__floor__() * (1 if v >= 0 else -1) for v in vals[k])
+        assert out[k] == float(Fraction(exact, 2 ** 128)), k
+    assert out[4] == 507
+    acc[_lib.ACC_LIMBS] = 1                                          # an out-of-range value in metric 0
+    assert np.isnan(engine.acc_value(acc).numpy()[0])
+
+
 def test_forward_status_without_gpu_reports_error_not_crash(lib):
     """rdn_forward_status synchronises the stream; on a host without a device it must fail cleanly."""
     rc = lib.rdn_forward_status(99, 0, 1, 100, None, 0, None)
     assert rc == -1 and b"unknown arch" in lib.rdn_last_error()
+    rc = lib.rdn_workspace_init(99, 0, 1, 100, None, 0, None)
+    assert rc == -1
 
 
 @pytest.mark.parametrize("arch", ARCHS)
@@ -313,7 +404,7 @@ def test_host_sanitizer_pack(arch, dtype, tmp_path):
             fh.write(t.tobytes())
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
     r = subprocess.run([os.path.join(csrc, "build", "asan", "host_check"), str(engine._arch(arch)),
-                        str(engine._dtype(dtype)), str(tmp_path / "t.bin"), str(tmp_path / "blob.bin")],
+                        str(engine.resolve_dtype(arch, dtype)), str(tmp_path / "t.bin"), str(tmp_path / "blob.bin")],
                        capture_output=True, text=True, env=env)
     assert r.returncode == 0, f"rc {r.returncode}: {r.stdout} {r.stderr}"
     assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr

@@ -184,3 +184,59 @@ def test_refgen_reproduces_reference_generator_bit_exact(inputs):
         np.testing.assert_array_equal(c.astype(np.float32), inputs[f"edge{L}_clean"])
     c, n, _, _ = generate_signals(1, signal_length=16384)
     np.testing.assert_array_equal(n.astype(np.float32), inputs["long_noisy"])
+
+
+def test_spike_recovery_reproduces_reference_statistics():
+    """tests/spike_stats.py on oracle.refgen (bit-exact with the reference generator) reproduces the
+    spike statistics make_golden.py --spikes recovered from the reference's own spectra exactly:
+    the recovery is deterministic and the GPU test compares like with like."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from oracle.refgen import generate_signals
+    from spike_stats import collect
+    with open(os.path.join(GOLDEN, "generator_stats.json")) as fh:
+        ref = json.load(fh)["spikes"]
+    np.random.seed(20250410 + 1)
+    clean, noisy, _, nstd = generate_signals(1000, extreme_noise_prob=1.0)
+    assert collect(clean, noisy, nstd[:, 0]) == ref
+
+
+def _acc_worker(rank, world, port, per, out):
+    import torch.distributed as dist
+    from raman_mi355x import _lib, engine
+    from raman_mi355x.distributed import shard
+    from test_abi import _acc_of
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    lo, hi = shard(per.shape[0])
+    acc = torch.zeros(_lib.ACC_WORDS, dtype=torch.int64)
+    for k in range(4):
+        acc[k * _lib.ACC_STRIDE: k * _lib.ACC_STRIDE + _lib.ACC_LIMBS] = torch.tensor(_acc_of(per[lo:hi, k]))
+    acc[_lib.ACC_COUNT] = hi - lo
+    dist.all_reduce(acc, op=dist.ReduceOp.SUM)
+    if rank == 0:
+        out["sums"] = engine.acc_value(acc).tolist()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_exact_accumulator_allreduce_world2_gloo():
+    """Config 4's reduction: exact metric accumulators of two rank shards, all-reduced (int64 SUM over
+    gloo), give the same bits as one process over all spectra."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from raman_mi355x import _lib, engine
+    from test_abi import _acc_of
+    g = np.load(os.path.join(GOLDEN, "metrics.npz"))
+    per = g["per_spectrum"].astype(np.float64)
+    acc = torch.zeros(_lib.ACC_WORDS, dtype=torch.int64)
+    for k in range(4):
+        acc[k * _lib.ACC_STRIDE: k * _lib.ACC_STRIDE + _lib.ACC_LIMBS] = torch.tensor(_acc_of(per[:, k]))
+    acc[_lib.ACC_COUNT] = per.shape[0]
+    one = engine.acc_value(acc).tolist()
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_acc_worker, args=(2, port, per, out), nprocs=2, join=True)
+        two = out["sums"]
+    assert one == two
+    np.testing.assert_allclose(np.array(one[:4]) / one[4], per.mean(axis=0), rtol=1e-13)

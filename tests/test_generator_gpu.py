@@ -83,3 +83,34 @@ def test_statistics_match_reference():
     frac = spiked / n
     assert abs(frac - 0.05) < 4 * np.sqrt(0.05 * 0.95 / n) + 0.005, frac
     assert abs(frac - ref["spiked_fraction"]) < 0.03
+
+
+def test_spike_process_matches_reference():
+    """The spike process (数据集产生.py:50-62) on the device simulator with every spectrum spiked
+    (extreme_noise_prob = 1): spike count U{1,2,3}, width U{20..99}, start U{0..L-W-1}, amplitude/σ
+    U[5,15), sign Bernoulli(0.5) — χ² against the uniform contract (p = 0.001 bounds) and two-sample
+    χ² against the same statistics of 1000 reference-generated spectra (generator_stats.json
+    "spikes", make_golden.py --spikes), both recovered by tests/spike_stats.py."""
+    from spike_stats import chi2_two_sample, chi2_uniform, collect
+    with open(os.path.join(GOLDEN, "generator_stats.json")) as fh:
+        ref = json.load(fh)["spikes"]
+    n = 2000
+    c, x, s, sd = _gpu(n, first=5000, extreme_noise_prob=1.0)
+    st = collect(c, x, sd)
+    print({k: v for k, v in st.items()})
+    # every spectrum carries 1..3 spikes (a count outside means two edges coincided: rare)
+    assert st["count_hist"][0] + st["count_hist"][4] <= n // 200, st["count_hist"]
+    assert st["overlapped_spectra"] < 0.08 * n
+    bounds = {"count_hist": 13.8, "width_hist": 24.3, "amp_hist": 27.9, "start_hist": 27.9}   # chi2(dof) at p=1e-3
+    for key, bound in bounds.items():
+        h = st[key][1:4] if key == "count_hist" else st[key]
+        r = ref[key][1:4] if key == "count_hist" else ref[key]
+        u, t = chi2_uniform(h), chi2_two_sample(h, r)
+        print(f"{key}: chi2 vs uniform {u:.1f}, vs reference {t:.1f} (bound {bound})")
+        assert u < bound, (key, u)
+        assert t < bound, (key, t)
+    assert 20 <= st["width_min_max"][0] and st["width_min_max"][1] <= 99
+    p = st["sign_pos"] / st["sign_n"]
+    assert abs(p - 0.5) < 4 * np.sqrt(0.25 / st["sign_n"]), p
+    pr = ref["sign_pos"] / ref["sign_n"]
+    assert abs(p - pr) < 4 * np.sqrt(0.25 / st["sign_n"] + 0.25 / ref["sign_n"])

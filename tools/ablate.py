@@ -114,14 +114,14 @@ def run():
         return blob.to(dev)
 
     for dtype in sys.argv[2:] or ["bf16x3", "fp32"]:
-        code = engine.DTYPE_ID[dtype]
+        code = engine.resolve_dtype(aid, dtype)
         packed = {name: pack_with(lib, code) for name, lib in libs.items()}
         times = {k: [] for k in libs}
         outs = {}
         wss = {}
         for name, lib in libs.items():          # CBAM networks: the team kernel's workspace
             wsz = ctypes.c_size_t()
-            assert lib.rdn_workspace_size(aid, code, B, L, ctypes.byref(wsz)) == 0
+            assert lib.rdn_workspace_size(aid, code, B, L, ctypes.byref(wsz), None) == 0
             wss[name] = (torch.zeros(max(1, wsz.value), dtype=torch.uint8, device=dev), wsz.value)
         for rnd in range(4):
             for name, lib in libs.items():
@@ -191,7 +191,7 @@ def parity():
                     xn = torch.from_numpy(np.ascontiguousarray(input_array(inp, s_))).to(dev)
                     y = torch.empty_like(xn)
                     wsz = ctypes.c_size_t()
-                    lib.rdn_workspace_size(aid, code, xn.shape[0], xn.shape[1], ctypes.byref(wsz))
+                    lib.rdn_workspace_size(aid, code, xn.shape[0], xn.shape[1], ctypes.byref(wsz), None)
                     ws = torch.empty(max(1, wsz.value), dtype=torch.uint8, device=dev)
                     rc = lib.rdn_forward(aid, code, blob.data_ptr(), xn.data_ptr(), y.data_ptr(), xn.shape[0], xn.shape[1],
                                          ws.data_ptr(), wsz.value, torch.cuda.current_stream().cuda_stream)

@@ -111,6 +111,8 @@ def main():
                                  "threads": torch.get_num_threads(), "torch": torch.__version__}
     scale = float(np.abs(yr).max())
     rec["max_rel_output_diff_engine_vs_cpu"] = float(np.abs(y1[:ncpu] - yr).max()) / scale
+    rec["max_abs_output_diff_engine_vs_cpu"] = float(np.abs(y1[:ncpu] - yr).max())
+    rec["output_max_abs"] = scale
     pe = per_spectrum(y1[:ncpu], clean[:ncpu]).mean(axis=0)
     rec["max_rel_mean_diff_engine_vs_cpu"] = float(np.max(np.abs(pe - pr.mean(axis=0)) / np.abs(pr.mean(axis=0))))
     rec["max_rel_mean_diff_batched_vs_batch1"] = max(abs(got[k] - rec["engine_batch1_loop"]["means"][k]) /
@@ -118,6 +120,7 @@ def main():
     text = json.dumps(rec, indent=1)
     print(text)
     if args.out:
+        os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
         with open(args.out, "w") as fh:
             fh.write(text + "\n")
 

@@ -44,13 +44,13 @@ def main():
     host = [sd[k].detach().float().contiguous() for k in names]
     ptrs = (ctypes.c_void_p * len(host))(*[t.data_ptr() for t in host])
     numels = (ctypes.c_int64 * len(host))(*[t.numel() for t in host])
-    a, code = engine.ARCH_ID[arch], engine.DTYPE_ID[dtype]
+    a, code = engine.ARCH_ID[arch], engine.resolve_dtype(arch, dtype)
     size = ctypes.c_size_t()
     assert lib.rdn_packed_size(a, code, ctypes.byref(size)) == 0
     blob = torch.empty(size.value, dtype=torch.uint8)
     assert lib.rdn_pack(a, code, ptrs, numels, len(host), ctypes.c_void_p(blob.data_ptr()), size.value) == 0
     packed = blob.to(dev)
-    assert lib.rdn_workspace_size(a, code, B, L, ctypes.byref(size)) == 0
+    assert lib.rdn_workspace_size(a, code, B, L, ctypes.byref(size), None) == 0
     ws = torch.zeros(size.value, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
