@@ -61,6 +61,11 @@ def flops_per_spectrum(arch, L):
     return per_pos * L
 
 
+def progress(msg):
+    """One line per bench stage on stderr (the JSON line stays alone on stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _cpu_model_name():
     try:
         with open("/proc/cpuinfo") as fh:
@@ -97,6 +102,24 @@ def _weights(arch):
     return R.MODELS[arch]().state_dict(), "random init"
 
 
+def _cpu_quota():
+    """CPUs of this process's cgroup CPU quota (cgroup v2 cpu.max / v1 cfs), None if unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+            q = int(fh.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+            p = int(fh.read())
+        return None if q <= 0 else max(1, q // p)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(arch, L, seconds):
     """The reference CPU path, restated (oracle.models: the reference's fp32 PyTorch-CPU ops, pinned to
     the reference by the golden fixtures), in the evaulate.py:29-37 loop shape on the box's host cores:
@@ -107,7 +130,12 @@ def cpu_baseline(arch, L, seconds):
     os.cpu_count() reports the whole host).  Bounded: ~`seconds` per variant."""
     from oracle.metrics import per_spectrum
     from oracle.models import forward as oracle_forward
-    all_threads = os.cpu_count() or 1
+    ncpu = os.cpu_count() or 1
+    quota = _cpu_quota()
+    # torch.set_num_threads(os.cpu_count()) as BASELINE.md prescribes, capped at the CPUs this process
+    # may actually run on: the GPU box reports the whole host (256) but grants a 16-CPU quota, and 256
+    # threads on 16 CPUs ran one batch-1 RRCDNet forward in 22 s (round 3, DESIGN.md §5)
+    threads = min(ncpu, quota) if quota else ncpu
     sd, wsrc = _weights(arch)
     clean, noisy = _reference_inputs(64, L)
     xs = [torch.tensor(v, dtype=torch.float32).view(1, 1, -1) for v in noisy]
@@ -122,32 +150,30 @@ def cpu_baseline(arch, L, seconds):
             if el >= seconds and n >= 3:
                 return n, el
 
-    torch.set_num_threads(all_threads)
+    torch.set_num_threads(threads)
+    progress(f"cpu baseline: batch-1 loop at {threads} threads")
     n1, e1 = loop(lambda i: oracle_forward(arch, sd, xs[i % len(xs)]))
     n2, e2 = loop(lambda i: per_spectrum(oracle_forward(arch, sd, xs[i % len(xs)]).view(1, -1).numpy(),
                                          clean[i % len(xs)][None]))
+    progress("cpu baseline: batched-16 loop")
     xb = torch.tensor(noisy[:16], dtype=torch.float32).unsqueeze(1)
     n3, e3 = loop(lambda i: oracle_forward(arch, sd, xb))
-    t16 = min(16, all_threads)
-    torch.set_num_threads(t16)
-    n4, e4 = loop(lambda i: oracle_forward(arch, sd, xs[i % len(xs)]))
-    torch.set_num_threads(all_threads)
     try:
         avail = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         avail = None
-    return {"value": n1 / e1, "unit": "spectra/s", "cores": all_threads, "kind": "port",
+    return {"value": n1 / e1, "unit": "spectra/s", "cores": threads, "kind": "port",
             "sample": f"{n1} batch-1 fp32 {arch} forwards at L={L} ({e1:.1f} s), evaulate.py:29-32 loop shape, "
-                      f"oracle.models (the reference's ops) at torch.set_num_threads(os.cpu_count() = {all_threads}); "
-                      f"weights: {wsrc}; inputs: the reference generator (oracle.refgen, seed 20250410)",
+                      f"oracle.models (the reference's ops) at torch.set_num_threads({threads}) = min(os.cpu_count() "
+                      f"= {ncpu}, cgroup CPU quota = {quota}); weights: {wsrc}; inputs: the reference generator "
+                      "(oracle.refgen, seed 20250410)",
             "with_metrics_spectra_per_s": n2 / e2,
             "batched16_spectra_per_s": 16 * n3 / e3,
-            "threads16_spectra_per_s": n4 / e4,
-            "note": "batched-16 runs the oracle's functional forward on a (16,1,L) tensor: one oneDNN conv per layer "
-                    "over 16x the data, slower per spectrum than batch 1 on this host (cache-resident batch-1 "
-                    "activations: 64 x L x 4 B = 2.6 MB per layer vs 41 MB at batch 16)",
-            "host": {"cpu_model": _cpu_model_name(), "os_cpu_count": all_threads, "sched_affinity_cpus": avail,
-                     "torch": torch.__version__}}
+            "note": "batched-16 runs the oracle's functional forward on a (16,1,L) tensor: PyTorch-CPU's (oneDNN) "
+                    "batch-16 Conv1d is slower per spectrum than batch 1 at L = 10,000 on these hosts (3.5x on the "
+                    "build container at 8 threads); it is the reference's own batched path (RRCDNet/train.py:166)",
+            "host": {"cpu_model": _cpu_model_name(), "os_cpu_count": ncpu, "cgroup_cpu_quota": quota,
+                     "sched_affinity_cpus": avail, "torch": torch.__version__}}
 
 
 def batch1_latency(model, code, arch, L, dev, n=200):
@@ -266,6 +292,7 @@ def config_keys(R, engine, args, dev, stream, world, rank):
     models = {a: _model(R, a, args.dtype, dev)[0] for a in args.config4_archs.split(",")}
     evaluate_synthetic({a: m for a, m in models.items()}, world * 2, seed=args.seed, signal_length=L,
                        batch_size=2, device=dev)                                   # warm-up (pack, first launch)
+    progress(f"config 4: {total} spectra x {len(models)} networks")
     res = evaluate_synthetic(models, total, seed=args.seed, signal_length=L, batch_size=B4, device=dev)
     cfg4 = {"config": "BASELINE.json configs[3]", "total_spectra": total, "batch_per_gpu": B4,
             "dtype": args.dtype, "signal_length": L, "n_gpus": world,
@@ -280,6 +307,7 @@ def config_keys(R, engine, args, dev, stream, world, rank):
     if world > 1 or rank != 0:
         return out
     # config 2: 1DCNN fp32 on config2_n on-device spectra
+    progress(f"config 2: DenoiseCNN fp32, {args.config2_n} spectra")
     m2, src = _model(R, "DenoiseCNN", "fp32", dev)
     evaluate_synthetic({"DenoiseCNN": m2}, 4, seed=args.seed, signal_length=L, batch_size=4, device=dev)
     r2 = evaluate_synthetic({"DenoiseCNN": m2}, args.config2_n, seed=args.seed, signal_length=L,
@@ -296,6 +324,7 @@ def config_keys(R, engine, args, dev, stream, world, rank):
                       "note": "end to end (simulate -> forward -> metrics) over all spectra; roofline_frac from the "
                               "forward kernel alone (HIP events)"}
     # config 5: PIDN / APIDN at L = 16384, 'f16' and fp32, plus the f16-vs-fp32 gap on the same inputs
+    progress("config 5: PIDN / APIDN at L = 16384")
     L5 = 16384
     cfg5 = {"config": "BASELINE.json configs[4]", "signal_length": L5}
     for a in ("PIDN", "APIDN"):
@@ -391,6 +420,7 @@ def main():
     def step():
         engine.forward(args.arch, code, packed, x, out=y, check=False)
 
+    progress(f"headline: {args.arch} {args.dtype} batch {B}, {args.warmup} + {args.steps} steps")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -425,6 +455,7 @@ def main():
 
     variants = {}
     if not args.no_variants:
+        progress("variants")
         for dt in ("f16", "f16-plain", "f16f8", "bf16x3", "bf16-unsafe", "fp32"):
             if dt == args.dtype:
                 continue
@@ -447,10 +478,12 @@ def main():
 
     batch1 = None
     if not args.no_batch1 and rank == 0:
+        progress("batch-1 latency")
         batch1 = batch1_latency(model, code, args.arch, L, dev)
 
     pipeline = None
     if not args.no_pipeline:
+        progress("pipeline")
         # indices [0, world*B) fed the headline; each rank's pipeline block of 4*B indices follows,
         # disjoint across ranks (rank r once re-generated rank r+1's steps)
         pipeline = time_pipeline(engine, args.arch, code, packed, args.seed, world * B + rank * 4 * B, B, L,

@@ -853,7 +853,25 @@ using V = h16c::V;
 constexpr int WB16 = h16c::WB;
 constexpr int NT = h16c::NT;
 constexpr int EDGE16_BYTES = EDGE_ROWS * h16c::ROWB;        // one edge, f16 rows
+// RDN_T16_TAGGED (default): the hand-off carries its own completion -- every 4-byte word of a slot
+// travels as an 8-byte granule {word, tag} written by one sc1 store (tag = the CBAM's sequence
+// number + 1; the slots are zeroed before each launch), and a consumer polls the granules it needs
+// until every tag is current.  The producer neither drains its stores nor meets a counter, and the
+// consumer's poll IS its read (one memory round trip after the last producer's stores land instead
+// of drain + counter add + counter poll + slot loads: MI355X_MICROARCH.md handoff-1to1 vs
+// handoff-flag).  Slot = 64 channel sums (f32: each tile's sum of its fp32 lane partials, rounded
+// once) | 64 ordered maxima | 2 x EDGE_ROWS rows of u (f16) as 4-byte words.
+#ifndef RDN_T16_TAGGED
+#define RDN_T16_TAGGED 1
+#endif
+constexpr int G_SUM = 0, G_MAX = 64, G_EDGE = 128;               // granule indices within a slot
+constexpr bool RDN_T16_TAGGED_ON = RDN_T16_TAGGED;
+constexpr int EDGE16_WORDS = EDGE16_BYTES / 4;                   // 160 per edge
+#if RDN_T16_TAGGED
+constexpr int SLOT16_BYTES = (G_EDGE + 2 * EDGE16_WORDS) * 8;    // 448 granules = 3584 B
+#else
 constexpr int SLOT16_BYTES = STAT_BYTES + 2 * EDGE16_BYTES;
+#endif
 // CBAM scratch in BUF1
 constexpr int SC = h16c::BUF1;
 constexpr int RED16_OFF = SC;                                  // [4 row blocks][64] f32 sums, then u32 maxima
@@ -907,7 +925,7 @@ __device__ __forceinline__ float quarter_max(float v) {
 // per-channel sum / max of u (BUF0) over the tile's own positions and its edge rows -> slot (sc1);
 // arrive at the team counter
 __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& ta, char* slot, unsigned* ctr,
-                                          bool arrive, const h16c::ChanStats* pre) {
+                                          bool arrive, const h16c::ChanStats* pre, unsigned tag) {
   char* lds = tl.lds;
   const Lane ln;
   const int tid = h16c::tid();
@@ -950,6 +968,35 @@ __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& 
     }
   }
   __syncthreads();
+#if RDN_T16_TAGGED
+  // one store phase, no drain, no arrival: the statistics (wave 0: granules {f32 sum, tag} and
+  // {ordered max, tag}) and the edge rows (u, f16) for the neighbours (waves 1-2: two granules per
+  // 16-B sc1 store): block 0 = rows [2H - 5, 2H) (the left neighbour's rows [WB - 5, WB)), block 1 =
+  // rows [T, T + 5).  arrive = false (test knob) publishes nothing.
+  if (!arrive) return;
+  const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slot, 0, SLOT16_BYTES, 0x00020000);
+  if (tid < 64) {
+    const int c = tid;
+    double sv = 0.0;
+    unsigned m = 0;
+#pragma unroll
+    for (int k = 0; k < h16c::RB; ++k) {
+      sv += (double)rs[k * 64 + c];
+      m = max(m, rm[k * 64 + c]);
+    }
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint((float)sv), tag}, sr, 8 * (G_SUM + c), 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{m, tag}, sr, 8 * (G_MAX + c), 0, 16);
+  } else if (tid < 64 + 2 * EDGE_ROWS * 8) {
+    const int i = tid - 64, e = i / (EDGE_ROWS * 8), k = (i / 8) % EDGE_ROWS, g = i & 7;
+    const int r = e == 0 ? 2 * H - EDGE_ROWS + k : T + k;
+    const u32x4 v = *(const u32x4*)(lds + h16c::BUF0 + h16c::soff(r, g));
+    const int g0 = G_EDGE + e * EDGE16_WORDS + (k * 8 + g) * 4;
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v[0], tag, v[1], tag}, sr, 8 * g0, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v[2], tag, v[3], tag}, sr, 8 * g0 + 16, 0, 16);
+  }
+  (void)ctr;
+#else
   // one store phase: the statistics (wave 0) and the edge rows (u, f16) for the neighbours (waves
   // 1-2): block 0 = rows [2H - 5, 2H) (the left neighbour's rows [WB - 5, WB)), block 1 = rows
   // [T, T + 5); every storing wave drains its stores, the workgroup barrier, then the arrival
@@ -974,12 +1021,14 @@ __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& 
   if (tid < 64 + 2 * EDGE_ROWS * 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0 && arrive) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  (void)tag;
+#endif
 }
 
 // apply the CBAM whose statistics sit in the team's slots to u (BUF0): h = [identity +] u*ca*sa
 // [then ReLU], written over u; idv: the identity (LINEAR_SAVE layout) for res != RES_NONE
 __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta, const char* slots0, int cbam_slot,
-                                        bool bias, int res, const V* idv, Stamps& st) {
+                                        bool bias, int res, const V* idv, Stamps& st, unsigned tag) {
   char* lds = tl.lds;
   const Lane ln;
   const int tid = h16c::tid(), lane = tid & 63, w = ln.w;
@@ -993,6 +1042,96 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   const float b2 = bias ? cmisc[4 + lane] : 0.f;
   const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slots0, 0, ta.TT * SLOT16_BYTES, 0x00020000);
 
+#if RDN_T16_TAGGED
+  // the granules this thread needs, polled until every tag is `tag` (uniform loop: one workgroup
+  // vote per round): the halo refresh (threads < 80: u of rows [0, 5) from the left neighbour's
+  // block 1, rows [WB - 5, WB) from the right neighbour's block 0; first / last tile: no
+  // neighbour) and the spectrum's per-channel sums / maxima from the TT slots (thread (c, part):
+  // slots part + 8k), combined in a fixed order
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const int edge_e = tid / (EDGE_ROWS * 8), edge_k = (tid / 8) % EDGE_ROWS, edge_g = tid & 7;
+  int eoff = -1;
+  if (tid < 2 * EDGE_ROWS * 8) {
+    const int tile = (tl.base + ta.halo) / ta.T;
+    const int nb = edge_e == 0 ? tile - 1 : tile + 1;
+    if (nb >= 0 && nb < ta.TT)
+      eoff = nb * SLOT16_BYTES + 8 * (G_EDGE + (1 - edge_e) * EDGE16_WORDS + (edge_k * 8 + edge_g) * 4);
+  }
+  u32x4 ea = {0u, 0u, 0u, 0u}, eb = {0u, 0u, 0u, 0u};
+  bool edge_ok = eoff < 0;
+  double* pool = (double*)(lds + POOL_OFF);
+  {
+    const int c = tid & 63, part = tid >> 6;
+    constexpr int PER = 2, STEP = h16c::WAVES * PER;
+    const int nbatch = (ta.TT + STEP - 1) / STEP;
+    double sp = 0.0;
+    unsigned mp = 0;
+    bool failed = false;
+    for (int b = 0; b < nbatch; ++b) {
+      u32x2 sv[PER], mv[PER];
+      bool ok[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) ok[k] = part + STEP * b + h16c::WAVES * k >= ta.TT;
+      for (unsigned it = 0;; ++it) {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+          if (!ok[k]) {
+            const int off = (part + STEP * b + h16c::WAVES * k) * SLOT16_BYTES;
+            sv[k] = __builtin_amdgcn_raw_buffer_load_b64(sr, off + 8 * (G_SUM + c), 0, 16);
+            mv[k] = __builtin_amdgcn_raw_buffer_load_b64(sr, off + 8 * (G_MAX + c), 0, 16);
+          }
+        }
+        if (b == 0 && !edge_ok) {
+          ea = __builtin_amdgcn_raw_buffer_load_b128(sr, eoff, 0, 16);
+          eb = __builtin_amdgcn_raw_buffer_load_b128(sr, eoff + 16, 0, 16);
+        }
+        bool mine = true;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+          ok[k] = ok[k] || (sv[k][1] == tag && mv[k][1] == tag);
+          mine = mine && ok[k];
+        }
+        if (b == 0) {
+          edge_ok = edge_ok || (ea[1] == tag && ea[3] == tag && eb[1] == tag && eb[3] == tag);
+          mine = mine && edge_ok;
+        }
+        if (__syncthreads_and(mine)) break;
+        // a wait that exceeds SPIN_LIMIT rounds (a team member never published: co-residency
+        // broken) raises the error words; once they are up every wait falls through (NaN outputs)
+        if (failed || it > SPIN_LIMIT) {
+          if (tid == 0 && !failed) {
+            __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ta.err + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          failed = true;
+          break;
+        }
+        if ((it & 63) == 63 &&
+            __syncthreads_or(__hip_atomic_load(ta.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+          failed = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(RDN_TEAM_SLEEP);
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        if (part + STEP * b + h16c::WAVES * k < ta.TT) {
+          sp += (double)__uint_as_float(sv[k][0]);
+          mp = max(mp, mv[k][0]);
+        }
+      }
+    }
+    double* ps = (double*)(lds + SLP_OFF);
+    unsigned* pm = (unsigned*)(lds + SLP_OFF + 8 * 64 * 8);
+    ps[part * 64 + c] = sp;
+    pm[part * 64 + c] = mp;
+  }
+  if (eoff >= 0) {
+    const int r = edge_e == 0 ? edge_k : WB16 - EDGE_ROWS + edge_k;
+    *(u32x4*)(lds + h16c::BUF0 + h16c::soff(r, edge_g)) = u32x4{ea[0], ea[2], eb[0], eb[2]};
+  }
+  __syncthreads();
+#else
   // halo refresh, fetched first: u of rows [0, 5) from the left neighbour's block 1, rows
   // [WB - 5, WB) from the right neighbour's block 0 (first / last tile: no neighbour)
   const int edge_e = tid / (EDGE_ROWS * 8), edge_k = (tid / 8) % EDGE_ROWS, edge_g = tid & 7;
@@ -1043,6 +1182,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
     *(u32x4*)(lds + h16c::BUF0 + h16c::soff(r, edge_g)) = edge_u;
   }
   __syncthreads();
+#endif
   st(10);
   // channel attention, evaluated whole by every wave (no barrier): the pooled avg / max of channel
   // `lane` from the 8 partials in a fixed order, the 4 + 4 hidden units as sums over the 64 lanes
@@ -1185,11 +1325,13 @@ __device__ __forceinline__ void team16_spectra(char* lds, const uint8_t* blob, c
       char* mine = tslots + ((size_t)(nbar & 1) * ta.TT + tile) * SLOT16_BYTES;
       const bool skip = ta.force_miss > 0 && __builtin_amdgcn_workgroup_id_x() == 0 && nbar + 1 == (unsigned)ta.force_miss;
       st(1);
-      publish16(tl, ta, mine, ctr, !skip, pre);
+      publish16(tl, ta, mine, ctr, !skip, pre, nbar + 1);
       st(3);
+#if !RDN_T16_TAGGED
       team_wait(ta, ctr, (nbar + 1) * (unsigned)ta.TT);
+#endif
       st(4);
-      apply16(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT16_BYTES, slot, ADS, res, id, st);
+      apply16(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT16_BYTES, slot, ADS, res, id, st, nbar + 1);
       st(5);
       ++nbar;
     };
@@ -1363,6 +1505,9 @@ static hipError_t launch_team(int arch, int mode, const TeamGeo& g, const uint8_
   // the sticky word after it collects every launch's timeouts until cbam_status reads and clears it
   hipError_t e = hipMemsetAsync(ta.counters, 0, g.counters, stream);
   if (e == hipSuccess) e = hipMemsetAsync(ta.err, 0, 4, stream);
+  // the tagged hand-off (RDN_T16_TAGGED) starts from tag 0 in every slot granule: no granule of an
+  // earlier launch can carry a tag this launch waits for
+  if (e == hipSuccess && mode == MODE_P16 && cb::t16::RDN_T16_TAGGED_ON) e = hipMemsetAsync(ta.slots, 0, g.slots, stream);
   if (e != hipSuccess) return e;
   const int64_t teams = n < g.teams ? n : g.teams;    // never more teams than spectra
   ta.teams = (int)teams;

@@ -11,7 +11,7 @@ hard() { [ $1 -ne 0 ] && [ $1 -ne 1 ]; }
 for st in $stages; do
   case $st in
     new)
-      timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu \
+      timeout -k 10 600 python -u -m pytest -x -v -rP --timeout 200 --timeout-method thread -m gpu \
         tests/test_headline_gpu.py tests/test_pipeline_gpu.py tests/test_generator_gpu.py tests/test_evaluate_gpu.py \
         tests/test_bench_multirank_gpu.py > gpurun_out/pytest_new.log 2>&1
       rc=$?; echo "pytest new rc=$rc"; grep -E "PASSED|FAILED|ERROR|Error|assert|heldout|max-abs" gpurun_out/pytest_new.log | grep -v "^tests.*PASSED" | tail -30; tail -2 gpurun_out/pytest_new.log

@@ -29,7 +29,8 @@ VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "m32ld2": "-DRDN_H16_M32=1 -DRDN_H16_LDSTEP=2", "m32pf2": "-DRDN_H16_M32=1 -DRDN_H16_PF=2",
             "ord": "-DRDN_H16_LDORDER=1", "ordld3": "-DRDN_H16_LDORDER=1 -DRDN_H16_LDSTEP=3", "ordld2": "-DRDN_H16_LDORDER=1 -DRDN_H16_LDSTEP=2",
             "wsame": "-DRDN_ABLATE_WSAME", "whalf": "-DRDN_ABLATE_WHALF",
-            "sleep1": "-DRDN_TEAM_SLEEP=1", "sleep2": "-DRDN_TEAM_SLEEP=2"}
+            "sleep1": "-DRDN_TEAM_SLEEP=1", "sleep2": "-DRDN_TEAM_SLEEP=2", "untag": "-DRDN_T16_TAGGED=0",
+            "untag_stamps": "-DRDN_T16_TAGGED=0 -DRDN_TEAM_STAMPS=1", "sleep4": "-DRDN_TEAM_SLEEP=4"}
 
 
 def build():
@@ -158,7 +159,6 @@ def parity():
     dev = torch.device("cuda")
     dtype = sys.argv[2] if len(sys.argv) > 2 else "fp32"
     archs = sys.argv[3:] or ["RRCDNet", "DenoiseCNN", "PIDN", "DSDN", "ADSDN", "APIDN"]
-    code = engine.DTYPE_ID[dtype]
     inp = golden_inputs()
     for name in VARIANTS:
         path = os.path.join(OUT, f"lib_{name}.so")
@@ -172,6 +172,7 @@ def parity():
             getattr(lib, fn).restype = res
         for arch in archs:
             aid = engine._arch(arch)
+            code = engine.resolve_dtype(arch, dtype)
             g = load_golden(arch)
             for which in ["synth", "trained"]:
                 if which == "trained" and not any(k.startswith("w::") for k in g.files):
