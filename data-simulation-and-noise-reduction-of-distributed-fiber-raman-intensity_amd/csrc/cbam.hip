@@ -866,6 +866,9 @@ constexpr int EDGE16_BYTES = EDGE_ROWS * h16c::ROWB;        // one edge, f16 row
 #endif
 constexpr int G_SUM = 0, G_MAX = 64, G_EDGE = 128;               // granule indices within a slot
 constexpr bool RDN_T16_TAGGED_ON = RDN_T16_TAGGED;
+#ifndef RDN_T16_SA_LOCAL
+#define RDN_T16_SA_LOCAL 1
+#endif
 constexpr int EDGE16_WORDS = EDGE16_BYTES / 4;                   // 160 per edge
 #if RDN_T16_TAGGED
 constexpr int SLOT16_BYTES = (G_EDGE + 2 * EDGE16_WORDS) * 8;    // 448 granules = 3584 B
@@ -881,7 +884,23 @@ constexpr int CA16_OFF = POOL_OFF + 2 * 64 * 8;                // channel attent
 constexpr int SA16_OFF = CA16_OFF + 8 * 64 * 4;                // spatial attention per tile row
 constexpr int M1_OFF = SA16_OFF + WB16 * 4;                    // [mean_c; max_c] map, rows -3 .. WB + 2
 constexpr int M2_OFF = M1_OFF + (WB16 + 8) * 4;
-static_assert(M2_OFF + (WB16 + 8) * 4 <= (int)h16c::LDS_BYTES, "CBAM scratch fits BUF1");
+constexpr int VOTE16_OFF = M2_OFF + (WB16 + 8) * 4;           // [2][8] u32 workgroup votes (wg_all)
+static_assert(VOTE16_OFF + 2 * 8 * 4 <= (int)h16c::LDS_BYTES, "CBAM scratch fits BUF1");
+
+// Workgroup-wide AND of a per-thread predicate: a wave ballot, one LDS word per wave (two parity
+// sets, so a vote needs one barrier), read back by every thread.  (__syncthreads_and would declare
+// static LDS, which a kernel holding all 160 KiB dynamically cannot have.)
+__device__ __forceinline__ bool wg_all(char* lds, bool v, unsigned& parity) {
+  unsigned* vote = (unsigned*)(lds + VOTE16_OFF) + 8 * (parity & 1);
+  const bool wave_ok = __builtin_amdgcn_ballot_w64(v) == ~0ull;
+  if ((h16c::tid() & 63) == 0) vote[h16c::tid() >> 6] = wave_ok ? 1u : 0u;
+  __syncthreads();
+  bool all = true;
+#pragma unroll
+  for (int k = 0; k < h16c::WAVES; ++k) all = all && vote[k] != 0;
+  ++parity;
+  return all;
+}
 
 struct Lane {             // this lane's (row, slot) items of the pointwise passes
   int w, h, rb, q, c16;
@@ -1067,6 +1086,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
     double sp = 0.0;
     unsigned mp = 0;
     bool failed = false;
+    unsigned vparity = 0;
     for (int b = 0; b < nbatch; ++b) {
       u32x2 sv[PER], mv[PER];
       bool ok[PER];
@@ -1095,7 +1115,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
           edge_ok = edge_ok || (ea[1] == tag && ea[3] == tag && eb[1] == tag && eb[3] == tag);
           mine = mine && edge_ok;
         }
-        if (__syncthreads_and(mine)) break;
+        if (wg_all(lds, mine, vparity)) break;
         // a wait that exceeds SPIN_LIMIT rounds (a team member never published: co-residency
         // broken) raises the error words; once they are up every wait falls through (NaN outputs)
         if (failed || it > SPIN_LIMIT) {
@@ -1107,7 +1127,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
           break;
         }
         if ((it & 63) == 63 &&
-            __syncthreads_or(__hip_atomic_load(ta.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+            !wg_all(lds, __hip_atomic_load(ta.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0, vparity)) {
           failed = true;
           break;
         }
@@ -1231,6 +1251,63 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   float* m2 = (float*)(lds + M2_OFF) + 3;      // the tile and [0, L)
   constexpr int SROWS = WB16 / h16c::WAVES;    // 80 rows per wave
   static_assert(SROWS % 16 == 0, "whole 16-row groups per wave");
+#if RDN_T16_SA_LOCAL
+  // RDN_T16_SA_LOCAL (default): each wave also forms [mean; max] of the 3 + 3 rows around its own
+  // 80 (one extra 16-lane group, lanes c16 < 6; rows outside the tile are 0) and then runs the conv7
+  // of its own rows from its own LDS writes (in order within a wave): no workgroup barrier and no
+  // separate pass between the spatial statistics and sa.  A halo row is written by two waves with
+  // the same value.
+  float* sa = (float*)(lds + SA16_OFF);
+  {
+    constexpr int KG = SROWS / 16;
+    auto srow = [&](int k) {                   // row of group k for this lane (k == KG: the halo group)
+      return k < KG ? SROWS * w + ln.c16 + 16 * k
+                    : (ln.c16 < 3 ? SROWS * w - 3 + ln.c16 : SROWS * w + SROWS + min(ln.c16, 5) - 3);
+    };
+    V ua[KG + 1], ub[KG + 1];
+#pragma unroll
+    for (int k = 0; k <= KG; ++k) {
+      const int r = min(max(srow(k), 0), WB16 - 1);
+      ua[k] = *(const V*)(lds + h16c::BUF0 + h16c::soff(r, ln.q));
+      ub[k] = *(const V*)(lds + h16c::BUF0 + h16c::soff(r, ln.q + 4));
+    }
+#pragma unroll
+    for (int k = 0; k <= KG; ++k) {
+      const V va = ua[k] * cq0, vb = ub[k] * cq4;
+      const V vs = va + vb, vm = __builtin_elementwise_max(va, vb);
+      const h2 s2 = (__builtin_shufflevector(vs, vs, 0, 1) + __builtin_shufflevector(vs, vs, 2, 3)) +
+                    (__builtin_shufflevector(vs, vs, 4, 5) + __builtin_shufflevector(vs, vs, 6, 7));
+      const h2 x2 = __builtin_elementwise_max(
+          __builtin_elementwise_max(__builtin_shufflevector(vm, vm, 0, 1), __builtin_shufflevector(vm, vm, 2, 3)),
+          __builtin_elementwise_max(__builtin_shufflevector(vm, vm, 4, 5), __builtin_shufflevector(vm, vm, 6, 7)));
+      const float sm = quarter_sum((float)s2[0] + (float)s2[1]);
+      const float mx = quarter_max(fmaxf((float)x2[0], (float)x2[1]));
+      if (ln.q == 0 && (k < KG || ln.c16 < 6)) {
+        const int r = srow(k);
+        const bool in = r >= 0 && r < WB16 && h16c::in_range(tl.base + r, tl.L);
+        m1[r] = in ? sm * (1.0f / 64.0f) : 0.f;
+        m2[r] = in ? mx : 0.f;
+      }
+    }
+    // sa = sigmoid(conv7([mean_c; max_c])) of this wave's rows
+#pragma unroll
+    for (int i = 0; i < (SROWS + 63) / 64; ++i) {
+      const int j = lane + 64 * i;
+      if (j < SROWS) {
+        const int r = SROWS * w + j;
+        float a = bias ? cmisc[82] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+          a = fmaf(cmisc[68 + k], m1[r + k - 3], a);
+          a = fmaf(cmisc[75 + k], m2[r + k - 3], a);
+        }
+        sa[r] = sigm(a);
+      }
+    }
+  }
+  __syncthreads();
+  st(12);
+#else
   {
     V ua[SROWS / 16], ub[SROWS / 16];
 #pragma unroll
@@ -1278,6 +1355,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   }
   __syncthreads();
   st(13);
+#endif
   V uv[NT];
   // h = [identity +] u*ca*sa [relu], in place, packed f16; rows outside [0, L) zero
   float sv[NT];
@@ -1439,7 +1517,10 @@ static int team_mode(int dtype) { return dtype == F16 ? MODE_P16 : dtype_mode(dt
 // co-resident workgroups per CU of the team kernel on `dev` (0 on any failure)
 static int team_blocks_per_cu(int arch, int mode, int dev) {
   const void* k = team_fn(arch, mode);
-  if (ensure_dynamic_lds(k, team_slot(arch, mode), team_lds(mode), dev) != hipSuccess) return 0;
+  if (ensure_dynamic_lds(k, team_slot(arch, mode), team_lds(mode), dev) != hipSuccess) {
+    (void)hipGetLastError();          // no team geometry (the segment path runs); leave no sticky error behind
+    return 0;
+  }
   int cur = 0, nb = 0;
   if (hipGetDevice(&cur) != hipSuccess) return 0;
   if (cur != dev && hipSetDevice(dev) != hipSuccess) return 0;

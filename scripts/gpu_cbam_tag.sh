@@ -15,7 +15,7 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 done
 done
 for a in ADSDN APIDN; do
-ABLATE_ONLY=${ABLATE_ONLY:-base,untag,sleep2} RDN_ABLATE_ARCH=$a timeout -k 10 300 python -u tools/ablate.py run f16 > gpurun_out/r03/ablate_$a.log 2>&1
+ABLATE_ONLY=${ABLATE_ONLY:-base,untag,saglobal,untag_saglobal,sleep2} RDN_ABLATE_ARCH=$a timeout -k 10 300 python -u tools/ablate.py run f16 > gpurun_out/r03/ablate_$a.log 2>&1
 rc=$?; echo "ablate $a rc=$rc"; grep -v amdgpu.ids gpurun_out/r03/ablate_$a.log | tail -4
 if [ $rc -ne 0 ]; then exit $rc; fi
 done
