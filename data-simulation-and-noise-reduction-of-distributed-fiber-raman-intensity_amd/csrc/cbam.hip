@@ -866,8 +866,11 @@ constexpr int EDGE16_BYTES = EDGE_ROWS * h16c::ROWB;        // one edge, f16 row
 #endif
 constexpr int G_SUM = 0, G_MAX = 64, G_EDGE = 128;               // granule indices within a slot
 constexpr bool RDN_T16_TAGGED_ON = RDN_T16_TAGGED;
+// RDN_T16_SA_LOCAL=1: per-wave conv7 with recomputed halo rows instead of a separate pass (one
+// barrier fewer): measured 0.4 % (ADSDN) / 2 % (APIDN) SLOWER with the tagged hand-off (the extra
+// 16-lane group and the wave-serial conv7 cost more than the barrier), so off
 #ifndef RDN_T16_SA_LOCAL
-#define RDN_T16_SA_LOCAL 1
+#define RDN_T16_SA_LOCAL 0
 #endif
 constexpr int EDGE16_WORDS = EDGE16_BYTES / 4;                   // 160 per edge
 #if RDN_T16_TAGGED
@@ -1252,7 +1255,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   constexpr int SROWS = WB16 / h16c::WAVES;    // 80 rows per wave
   static_assert(SROWS % 16 == 0, "whole 16-row groups per wave");
 #if RDN_T16_SA_LOCAL
-  // RDN_T16_SA_LOCAL (default): each wave also forms [mean; max] of the 3 + 3 rows around its own
+  // RDN_T16_SA_LOCAL: each wave also forms [mean; max] of the 3 + 3 rows around its own
   // 80 (one extra 16-lane group, lanes c16 < 6; rows outside the tile are 0) and then runs the conv7
   // of its own rows from its own LDS writes (in order within a wave): no workgroup barrier and no
   // separate pass between the spatial statistics and sa.  A halo row is written by two waves with
