@@ -17,6 +17,7 @@ per network at the end (engine.Workspace), not per batch.  ``write_metrics`` pro
 evaulate.py:78-80's ``metrics.txt`` format.
 """
 import os
+import sys
 import time
 from datetime import datetime
 
@@ -99,12 +100,14 @@ def evaluate(model, noisy_data, clean_data, batch_size=1024, device=None):
 
 
 def evaluate_synthetic(models, total, seed=20250410, signal_length=10000, batch_size=8192, device=None,
-                       first_index=0, gen_kwargs=None, sync_timing=True):
+                       first_index=0, gen_kwargs=None, log_every_s=0.0):
     """Config 4: ``total`` simulator spectra [first_index, first_index + total),
     sharded over the ranks as [r·N/W, (r+1)·N/W), each chunk generated on the device, denoised by
     every model in ``models`` (name -> module) and metered into that model's exact accumulator.
     Returns {name: {"means", "spectra", "seconds", "spectra_per_s"}} with the all-reduced means
-    (identical for any world size) and the max-over-ranks wall time of the loop."""
+    (identical for any world size) and the max-over-ranks wall time of the loop.  ``log_every_s`` > 0
+    prints progress to stderr about that often (the loop then waits for the device every 64 chunks,
+    so the printed count is what the GPU has finished)."""
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device())
     device = torch.device(device)
@@ -127,7 +130,14 @@ def evaluate_synthetic(models, total, seed=20250410, signal_length=10000, batch_
                 dist.barrier()
             torch.cuda.synchronize(device)
             t0 = time.perf_counter()
-            for b0 in range(lo, hi, B):
+            t_log = t0
+            for i, b0 in enumerate(range(lo, hi, B)):
+                if log_every_s > 0 and i % 64 == 63:
+                    torch.cuda.synchronize(device)
+                    if time.perf_counter() - t_log >= log_every_s:
+                        t_log = time.perf_counter()
+                        print(f"[evaluate_synthetic rank {rank}] {name}: {b0 - lo} / {hi - lo} spectra, "
+                              f"{t_log - t0:.1f} s", file=sys.stderr, flush=True)
                 nb = min(B, hi - b0)
                 engine.generate(nb, seed, first_index=first_index + b0, signal_length=L, device=device,
                                 out=(clean[:nb], noisy[:nb]), **gen_kwargs)

@@ -65,7 +65,7 @@ def main():
         models[a] = m.to(dev).eval().set_engine_dtype(args.dtype)
     evaluate_synthetic(models, 2 * W, seed=args.seed, signal_length=args.L, batch_size=2, device=dev)   # warm-up
     res = evaluate_synthetic(models, args.total, seed=args.seed, signal_length=args.L, batch_size=args.batch,
-                             device=dev)
+                             device=dev, log_every_s=30.0)
     if rank == 0:
         rec = {"config": "BASELINE.json configs[3]", "total_spectra": args.total, "n_gpus": W,
                "dist_backend": args.dist_backend if distributed else None, "dtype": args.dtype, "L": args.L,
