@@ -47,10 +47,13 @@ CONFIG_OF = {"DenoiseCNN": 1, "RRCDNet": 2, "DSDN": 3, "ADSDN": 3, "PIDN": 4, "A
 
 
 def mfma_cost(arch, dtype):
-    """bf16-MFMA units executed per algorithmic product: RDN_F16MIX (Python 'f16' on RRCDNet) runs 3 of
-    its 29 big layers with the e4m3 correction (2 units) and the rest plain (1)."""
+    """bf16-MFMA units executed per algorithmic product: RDN_F16MIX (Python 'f16' on RRCDNet) runs the
+    layers of its correction mask with the e4m3 correction (2 units) and the rest plain (1)."""
     if dtype == "f16" and arch == "RRCDNet":
-        return (26 + 3 * 2) / 29
+        from raman_mi355x import engine
+        k = bin(engine.default_correction_mask(arch)).count("1")
+        big = LAYERS[arch][0]
+        return (big - k + 2 * k) / big
     return MFMA_COST.get(dtype)
 
 

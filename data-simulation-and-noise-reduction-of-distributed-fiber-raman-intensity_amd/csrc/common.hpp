@@ -35,6 +35,12 @@ constexpr size_t SMALL_BYTES = SMALL_SLOTS * SMALL_SLOT_FLOATS * sizeof(float); 
 // slot 63 word 0/1: 64-bit per-layer correction mask of the f16 + e4m3 layout (bit i = big layer i
 // consumes the e4m3 correction): all ones for RDN_F16F8, a calibrated subset for RDN_F16MIX
 constexpr int CORR_SLOT = 63;
+// RDN_F16MIX (RRCDNet): the last RDN_F16MIX_TAIL right-branch layers (of 15) keep the e4m3
+// correction (pack.cpp f16mix_default_mask, fused_inplace.hip rrcdnet_hybrid)
+#ifndef RDN_F16MIX_TAIL
+#define RDN_F16MIX_TAIL 3
+#endif
+constexpr int F16MIX_TAIL = RDN_F16MIX_TAIL;
 // slot 63 word 2: layout tag BLOB_MAGIC | arch << 8 | dtype, written by rdn_pack for every dtype
 // (include/raman_mi355x.h RDN_BLOB_MAGIC); the RDN_F16MIX kernels check it before reading the blob
 constexpr uint32_t BLOB_MAGIC = 0x52440000u;

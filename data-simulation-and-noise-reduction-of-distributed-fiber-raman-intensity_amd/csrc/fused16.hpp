@@ -87,6 +87,13 @@ constexpr int BIAS_OFF = H16_BIAS_OFF;
 #ifndef RDN_H16_M32
 #define RDN_H16_M32 0
 #endif
+// RDN_H16_EDGE_POST: a tile holding positions outside [0, L) stores its layer outputs unmasked (the
+// MFMA loop is the interior tiles' own) and each wave then zeroes its rows outside [0, L) -- a few
+// stores after the loop, before the barrier; 0 = a per-lane range check and select in every epilogue
+// (the edge tiles of a spectrum then ran ~10 % slower: the CBAM team kernel waits for them)
+#ifndef RDN_H16_EDGE_POST
+#define RDN_H16_EDGE_POST 1
+#endif
 constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
 constexpr int MH = 2;                                 // output-channel halves (32 channels each)
@@ -365,6 +372,18 @@ struct ChanStats {
   int lo, hi;
 };
 
+// Rows of this wave's block [r0, r0 + RW) at spectrum positions outside [0, L): its channel half
+// (slots 4h .. 4h + 3) set to zero (the Conv1d zero padding of the next layer's input)
+__device__ __forceinline__ void zero_outside(const Tile& tl, uint32_t dst, int r0, int h, int lane) {
+  const int front = min(RW, max(0, -tl.base - r0));                 // rows at positions < 0
+  const int back = max(front, min(RW, tl.L - tl.base - r0));       // first row at a position >= L
+  const int nb = front + (RW - back);
+  for (int i = lane; i < 4 * nb; i += 64) {
+    const int k = i >> 2, r = r0 + (k < front ? k : back + (k - front));
+    *(V*)(tl.lds + dst + soff(r, 4 * h + (i & 3))) = (V)((E)0);
+  }
+}
+
 template <int EPI, bool EDGE>
 __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int dil, const Frags& F, Frags& G,
                                       bool has_next = true, V* idv = nullptr, ChanStats* cs = nullptr) {
@@ -419,14 +438,17 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   // 0-3, 8-11 are slot 4h + e, regs 4-7, 12-15 slot 4h + 2 + e (h16_channel order)
   const int sa0 = (int)dst + (h ? tl.koff[2][2] : tl.koff[2][0]), sa1 = (int)dst + (h ? tl.koff[2][3] : tl.koff[2][1]);
   auto epilogue = [&](int n, const Acc& a) {
-    const bool valid = !EDGE || in_range(pos0 + NR * n + (lane & 31), tl.L);
+    const bool valid = !EDGE || RDN_H16_EDGE_POST || in_range(pos0 + NR * n + (lane & 31), tl.L);
     store_slot((V*)(tl.lds + sa0 + n * NR * ROWB), __builtin_shufflevector(a.v, a.v, 0, 1, 2, 3, 8, 9, 10, 11), valid);
     store_slot((V*)(tl.lds + sa1 + n * NR * ROWB), __builtin_shufflevector(a.v, a.v, 4, 5, 6, 7, 12, 13, 14, 15), valid);
   };
 #else
   const int sa = (int)dst + (h ? tl.koff[2][1] : tl.koff[2][0]);     // slot 4h + q of row r0
   auto epilogue = [&](int n, const Acc& a) {
-    const bool valid = !EDGE || in_range(pos0 + NR * n + (lane & 15), tl.L);
+    // positions outside [0, L): only the N-tiles that straddle 0 or L (a wave-uniform, scalar test)
+    // pay the per-lane check and select; the other N-tiles of an edge tile store unmasked
+    bool valid = true;
+    if constexpr (EDGE && !RDN_H16_EDGE_POST) valid = in_range(pos0 + NR * n + (lane & 15), tl.L);
     V* p = (V*)(tl.lds + sa + n * NR * ROWB);
     if constexpr (EPI == LINEAR_SAVE) idv[n] = *p;
     const f32x8 v = __builtin_shufflevector(a.v[0], a.v[1], 0, 1, 2, 3, 4, 5, 6, 7);
@@ -472,6 +494,7 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     prev = acc;
   }
   epilogue(NT - 1, prev);
+  if constexpr (EDGE && RDN_H16_EDGE_POST) zero_outside(tl, dst, pos0 - tl.base, h, lane);
   tl.layer += 1;
 #if defined(RDN_ABLATE_NOBARRIER)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

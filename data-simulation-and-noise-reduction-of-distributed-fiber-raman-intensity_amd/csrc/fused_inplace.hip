@@ -180,7 +180,7 @@ IP_BODY(pidn) {
 #define RDN_IP_PRIO 0
 #endif
 // RDN_F16MIX: corrected layers at the end of RRCDNet's right branch (pack.cpp f16mix_default_mask)
-constexpr int RRCDNET_F16MIX_TAIL = 3;
+constexpr int RRCDNET_F16MIX_TAIL = F16MIX_TAIL;
 
 // RDN_F16MIX on full tiles: the plain f16 layers run on fused16's ping-pong tile (two 640 x 128-B
 // buffers, one barrier per layer, no write-back lag: 8 % fewer cycles per layer than the in-place

@@ -566,7 +566,7 @@ uint32_t get_blob_tag(const void* blob) {
 // correcting right_net.15-17 (big layers 12-14) brings it to 1.36e-2 with both heads split, 1.65e-2 with the left head in plain f16 (tools/f16mix_masks.py).  The
 // pattern is compiled into the kernel (fused_inplace.hip RRCDNET_F16MIX_TAIL); the blob records it.
 uint64_t f16mix_default_mask(int arch) {
-  return arch == RRCDNET ? (0x7ull << 12) : 0;
+  return arch == RRCDNET ? (((1ull << F16MIX_TAIL) - 1) << (15 - F16MIX_TAIL)) : 0;
 }
 void set_corr_mask(void* blob, uint64_t mask) {
   uint32_t* w = (uint32_t*)((uint8_t*)blob + (size_t)CORR_SLOT * SMALL_SLOT_FLOATS * 4);

@@ -31,17 +31,24 @@ __device__ __forceinline__ void rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   using HO = HeadOut<MODE_H8, NBK>;
   int n16;
   PPNS::Tile t16 = PPNS::make_tile(tl.lds, blob, x, L, T, tiles, H, n16);
-  static_assert(PP % 2 == 1, "the ping-pong run ends on F0 -> BUF1");
   PPNS::Frags F0, F1;            // alternating operand buffers (fused16.hpp layer)
   PPNS::load_frags(t16, 0, F0);
   PPNS::stem(t16, 0, PPNS::BUF0);
   PPNS::lds_barrier();
-  for (int i = 0; i < PP / 2; ++i) {
+  for (int i = 0; i < (PP - 1) / 2; ++i) {
     PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1);
     PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF1, PPNS::BUF0, 1, F1, F0);
   }
-  PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1, false);
-  uint32_t cur = PPNS::BUF1;
+  // the last ping-pong layer (no next-layer operands: the in-place engine loads its own)
+  uint32_t cur;
+  if constexpr (PP % 2 == 1) {
+    PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1, false);
+    cur = PPNS::BUF1;
+  } else {
+    PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1);
+    PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF1, PPNS::BUF0, 1, F1, F0, false);
+    cur = PPNS::BUF0;
+  }
   f32x4 id[16 * NBK / 4];
   LayerA<MODE_H8> a;
   tl.layer = PP;

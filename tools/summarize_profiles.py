@@ -1,6 +1,7 @@
 """Summarise a scripts/gpu_profile.sh run into the committed evidence under profiles/.
 
-    python tools/summarize_profiles.py gpurun_out/prof profiles/r01
+    python tools/summarize_profiles.py gpurun_out/prof profiles/r01       (scripts/gpu_profile.sh)
+    python tools/summarize_profiles.py gpurun_out/final profiles/r03      (scripts/gpu_final.sh)
 
 Writes <dst>/rocprof/kernel_stats_bench.csv (rocprofv3 --kernel-trace --stats of the default
 `python bench.py`), <dst>/rocprof/kernel_stats_by_grid.csv (the same trace per kernel AND grid size:
@@ -19,7 +20,37 @@ import sys
 
 KERNELS = {"f16": "rdn::ip::rrcdnet_hybrid<3>", "f16-plain": "rdn::h16f::rrcdnet", "f16f8": "rdn::ip::rrcdnet<3, 0>",
            "bf16x3": "rdn::ip::rrcdnet<2, 0>", "bf16-unsafe": "rdn::h16::rrcdnet"}
+# scripts/gpu_final.sh passes: pmc_<arch>-<dtype>_<counter>, batch per arch
+KERNELS_FINAL = {("RRCDNet", "f16"): ("rdn::ip::rrcdnet_hybrid<3>", 8192),
+                 ("RRCDNet", "f16-plain"): ("rdn::h16f::rrcdnet", 8192),
+                 ("ADSDN", "f16"): ("rdn::cb::team16_forward<true>", 2048),
+                 ("APIDN", "f16"): ("rdn::cb::team16_forward<false>", 2048)}
 BATCH = 8192          # bench.py default --batch (the PMC passes run the default batch)
+
+
+def kernel_ns(path, kernel):
+    """Mean duration (ns) of `kernel`'s dispatches in a pass run with --kernel-trace, or None."""
+    d = []
+    for f in glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if kernel in r["Kernel_Name"]:
+                    d.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return sum(d) / len(d) if d else None
+
+
+def derived(c, ns):
+    """Ratios the DESIGN cites: MFMA busy of SIMD cycles, VALU per MFMA, LDS conflict share, clock."""
+    out = {}
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "SQ_BUSY_CU_CYCLES" in c:
+        out["mfma_busy_frac_of_simd_cycles"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * c["SQ_BUSY_CU_CYCLES"])
+    if "SQ_INSTS_VALU" in c and c.get("SQ_INSTS_MFMA"):
+        out["valu_per_mfma"] = c["SQ_INSTS_VALU"] / c["SQ_INSTS_MFMA"]
+    if c.get("SQ_LDS_IDX_ACTIVE") and "SQ_LDS_BANK_CONFLICT" in c:
+        out["lds_conflict_frac_of_lds_active"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
+    if "GRBM_GUI_ACTIVE" in c and ns:
+        out["clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / ns
+    return out
 
 
 def counters(path, kernel):
@@ -79,14 +110,34 @@ def main():
         if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "SQ_BUSY_CU_CYCLES" in c:
             summary[f"RRCDNet/{dt}"]["mfma_busy_frac_of_simd_cycles"] = (
                 c["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * c["SQ_BUSY_CU_CYCLES"]))
+    for (arch, dt), (kern, batch) in KERNELS_FINAL.items():
+        c, ns = {}, None
+        for d in sorted(glob.glob(os.path.join(src, f"pmc_{arch}-{dt}_*"))):
+            if os.path.isdir(d):
+                c.update(counters(d, kern))
+                ns = ns or kernel_ns(d, kern)
+        if not c:
+            continue
+        rec = {"kernel": kern, "batch": batch, "per_dispatch": c, "kernel_ns_under_pmc": ns}
+        rec.update(derived(c, ns))
+        summary[f"{arch}/{dt}"] = rec
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            kib = 2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]
+            traffic[f"{arch}/{dt}"] = {
+                "bytes_per_spectrum": kib * 1024 / batch,
+                "source": f"{dst}/rocprof/pmc_summary.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+                          f"{kern}, batch {batch}, (2*FETCH_SIZE+WRITE_SIZE) KiB per dispatch / {batch}"}
+    for name in ("bench.json", "kt_bench.json"):
+        if os.path.exists(os.path.join(src, name)):
+            shutil.copy(os.path.join(src, name), os.path.join(dst, name.replace("kt_bench", "bench_under_rocprof")))
     with open(os.path.join(dst, "rocprof", "pmc_summary.json"), "w") as fh:
         json.dump(summary, fh, indent=1)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     if traffic:
         with open(os.path.join(root, "profiles", "traffic.json"), "w") as fh:
             json.dump(traffic, fh, indent=1)
-    print(json.dumps({"traffic": traffic, "mfma_busy": {k: v.get("mfma_busy_frac_of_simd_cycles") for k, v in summary.items()}},
-                     indent=1))
+    print(json.dumps({"traffic": traffic, "derived": {k: {kk: vv for kk, vv in v.items() if kk not in ("per_dispatch",)}
+                                                      for k, v in summary.items()}}, indent=1))
 
 
 if __name__ == "__main__":

@@ -64,6 +64,17 @@ def main():
     ms = e0.elapsed_time(e1)
     st = ws[-256 * NSTAMP * 8:].view(torch.int64).view(256, NSTAMP).cpu().double()
     used = st.sum(1) > 0
+    # per tile index (workgroup id % TT): the conv phase and the poll phase, to see which tiles of a
+    # team the others wait for (TT from L: 640-row tiles with 6-row halos)
+    tt = -(-L // 628)
+    wg = torch.arange(256)[used]
+    byt = {}
+    for i, g in zip(wg.tolist(), st[used]):
+        byt.setdefault(i % tt, []).append(g)
+    print("per tile: conv cycles / poll cycles (mean over teams)")
+    for t in sorted(byt):
+        g = torch.stack(byt[t])
+        print(f"  tile {t:2d}: conv {g[:, 1].mean():.4e}  poll {g[:, 10].mean() + g[:, 4].mean():.4e}")
     st = st[used]
     tot = st.sum(1)
     print(f"[{variant}] {arch} {dtype} L={L} B={B}: {ms:.2f} ms, {B / ms * 1e3:,.0f} spectra/s, {int(used.sum())} workgroups")
