@@ -1468,7 +1468,11 @@ __global__ __launch_bounds__(h16c::THREADS) void team16_forward(const uint8_t* _
   const int team = __builtin_amdgcn_workgroup_id_x() / ta.TT, tile = __builtin_amdgcn_workgroup_id_x() - team * ta.TT;
   const int base = tile * ta.T - ta.halo;
   // a tile holds positions outside [0, L) for every spectrum or for none (one L per launch)
+#if defined(RDN_ABLATE_ALLEDGE)          // diagnostic: every tile on the edge-tile code
+  if (false) t16::team16_spectra<ADS, false>(lds, blob, big16, x, y, L, ta, team, tile);
+#else
   if (base >= 0 && base + t16::WB16 <= L) t16::team16_spectra<ADS, false>(lds, blob, big16, x, y, L, ta, team, tile);
+#endif
   else t16::team16_spectra<ADS, true>(lds, blob, big16, x, y, L, ta, team, tile);
 }
 
