@@ -94,13 +94,7 @@ constexpr int BIAS_OFF = H16_BIAS_OFF;
 #ifndef RDN_H16_EDGE_POST
 #define RDN_H16_EDGE_POST 1
 #endif
-// H16_WAVES: waves per workgroup (8: one workgroup per CU, two waves per SIMD; 4 with a 320-row
-// tile: two workgroups per CU, the per-wave geometry -- 160 rows x 32 output channels -- unchanged)
-#ifdef H16_WAVES
-constexpr int WAVES = H16_WAVES;
-#else
 constexpr int WAVES = 8;
-#endif
 constexpr int THREADS = 64 * WAVES;
 constexpr int MH = 2;                                 // output-channel halves (32 channels each)
 constexpr int RB = WAVES / MH;                        // row blocks
