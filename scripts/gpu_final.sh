@@ -12,12 +12,12 @@ STAGES=${STAGES:-bench kt pmc}
 if [[ " $STAGES " == *" bench "* ]]; then
   timeout -k 10 600 python -u bench.py > $OUT/bench.log 2>&1
   rc=$?; echo "bench rc=$rc"; tail -1 $OUT/bench.log | cut -c1-400; if [ $rc -ne 0 ]; then exit $rc; fi
-  tail -1 $OUT/bench.log > $OUT/bench.json
+  grep "^{" $OUT/bench.log | tail -1 > $OUT/bench.json
 fi
 if [[ " $STAGES " == *" kt "* ]]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py --no-cpu-baseline --no-configs > $OUT/kt_bench.log 2>&1
   rc=$?; echo "kt rc=$rc"; tail -1 $OUT/kt_bench.log | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi
-  tail -1 $OUT/kt_bench.log > $OUT/kt_bench.json
+  grep "^{" $OUT/kt_bench.log | tail -1 > $OUT/kt_bench.json
 fi
 # PMC: the timed launches only (no batch-1 loop, variants, pipeline or configs)
 SHORT="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-variants --no-pipeline --no-batch1 --no-configs"

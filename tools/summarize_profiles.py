@@ -134,8 +134,14 @@ def main():
         json.dump(summary, fh, indent=1)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     if traffic:
-        with open(os.path.join(root, "profiles", "traffic.json"), "w") as fh:
-            json.dump(traffic, fh, indent=1)
+        tpath = os.path.join(root, "profiles", "traffic.json")
+        merged = {}
+        if os.path.exists(tpath):            # keep the entries this run did not re-measure
+            with open(tpath) as fh:
+                merged = json.load(fh)
+        merged.update(traffic)
+        with open(tpath, "w") as fh:
+            json.dump(merged, fh, indent=1)
     print(json.dumps({"traffic": traffic, "derived": {k: {kk: vv for kk, vv in v.items() if kk not in ("per_dispatch",)}
                                                       for k, v in summary.items()}}, indent=1))
 
