@@ -63,6 +63,12 @@ __device__ __forceinline__ float ord2f(unsigned o) {
   return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
 __device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + expf(-v)); }
+// sigmoid from v_exp_f32 (2^x) and v_rcp_f32 (~1 ulp each): the f16 team kernel's channel / spatial
+// attention, which it rounds to f16 before use (the fp32 kernels and every network output use sigm);
+// exp2 overflow gives rcp(inf) = 0 = sigmoid(-inf)
+__device__ __forceinline__ float sigm_fast(float v) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v));
+}
 
 // LDS scratch behind the activation buffer
 constexpr int S1_OFF = ACT_BYTES_F32;                 // mean_c(u*ca) for rows -3 .. 514   (518 f32)
@@ -307,7 +313,7 @@ constexpr int SLOT_BYTES = STAT_BYTES + 2 * EDGE_BYTES;   // + the tile's first 
 static_assert(2 * TEAM_HALO - EDGE_ROWS >= TEAM_HALO - 1 && TEAM_HALO >= 4, "edge rows lie in the tile's own rows");
 constexpr unsigned SPIN_LIMIT = 1u << 22;          // ~0.3 s of s_sleep polls
 #ifndef RDN_TEAM_SLEEP
-#define RDN_TEAM_SLEEP 8                           // s_sleep units (64 clocks) between two polls
+#define RDN_TEAM_SLEEP 2                           // s_sleep units (64 clocks) between two polls
 #endif
 constexpr int TEAM_CTR_STRIDE = 16;                // u32s between team counters (64 B)
 
@@ -1081,11 +1087,14 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   }
   u32x4 ea = {0u, 0u, 0u, 0u}, eb = {0u, 0u, 0u, 0u};
   bool edge_ok = eoff < 0;
-  double* pool = (double*)(lds + POOL_OFF);
   {
     const int c = tid & 63, part = tid >> 6;
     constexpr int PER = 2, STEP = h16c::WAVES * PER;
     const int nbatch = (ta.TT + STEP - 1) / STEP;
+    // this tile's own slot is not polled: its granules are the values publish16 stored, recomputed
+    // from the same LDS partials in the same order (same bits), so the last tile to publish goes on
+    // without a round trip through memory for its own statistics
+    const int own = (tl.base + ta.halo) / ta.T;
     double sp = 0.0;
     unsigned mp = 0;
     bool failed = false;
@@ -1094,7 +1103,23 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
       u32x2 sv[PER], mv[PER];
       bool ok[PER];
 #pragma unroll
-      for (int k = 0; k < PER; ++k) ok[k] = part + STEP * b + h16c::WAVES * k >= ta.TT;
+      for (int k = 0; k < PER; ++k) {
+        const int t = part + STEP * b + h16c::WAVES * k;
+        ok[k] = t >= ta.TT || t == own;
+        if (t == own) {
+          const float* rs = (const float*)(lds + RED16_OFF);
+          const unsigned* rm = (const unsigned*)(lds + RED16_OFF + 4 * 64 * 4);
+          double s0 = 0.0;
+          unsigned m0 = 0;
+#pragma unroll
+          for (int j = 0; j < h16c::RB; ++j) {
+            s0 += (double)rs[j * 64 + c];
+            m0 = max(m0, rm[j * 64 + c]);
+          }
+          sv[k] = u32x2{__float_as_uint((float)s0), tag};
+          mv[k] = u32x2{m0, tag};
+        }
+      }
       for (unsigned it = 0;; ++it) {
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
@@ -1220,7 +1245,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
       sum += ps[k * 64 + lane];
       m = max(m, pm[k * 64 + lane]);
     }
-    const float pa = (float)(sum / (double)tl.L), px = ord2f(m);
+    const float pa = (float)sum * __builtin_amdgcn_rcpf((float)tl.L), px = ord2f(m);
     float oa = b2, om = b2;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1230,7 +1255,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
       oa = fmaf(cw2v[j], ha, oa);
       om = fmaf(cw2v[j], hm, om);
     }
-    cav = sigm(oa + om);
+    cav = sigm_fast(oa + om);
   }
   // this lane's 8 channels of ca through the wave's own LDS row (in-order within a wave)
   float* caw = (float*)(lds + CA16_OFF) + 64 * w;
@@ -1243,13 +1268,14 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   // [mean; max] completes inside one wave; partial sums / maxima to f32
   char* b0 = lds + h16c::BUF0 + (ln.h ? tl.koff[2][1] : tl.koff[2][0]);
   typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-  V cah, cq0, cq4;           // ca of this lane's pointwise slot; of slots q and q + 4
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    cah[j] = (_Float16)caw[h16_channel(ln.slot(), j)];
-    cq0[j] = (_Float16)caw[h16_channel(ln.q, j)];
-    cq4[j] = (_Float16)caw[h16_channel(ln.q + 4, j)];
-  }
+  // ca of this lane's pointwise slot; of slots q and q + 4 (h16_channel(g, j): channels j < 4 and
+  // j >= 4 are 4 consecutive channels each, so two 16-B LDS reads per slot)
+  auto ca_slot = [&](int g) {
+    const int c0 = h16_channel(g, 0);
+    const f32x4 lo = *(const f32x4*)(caw + c0), hi = *(const f32x4*)(caw + c0 + 16);
+    return __builtin_convertvector(__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7), V);
+  };
+  const V cah = ca_slot(ln.slot()), cq0 = ca_slot(ln.q), cq4 = ca_slot(ln.q + 4);
   float* m1 = (float*)(lds + M1_OFF) + 3;      // [mean_c; max_c] of rows -3 .. WB + 2, zero outside
   float* m2 = (float*)(lds + M2_OFF) + 3;      // the tile and [0, L)
   constexpr int SROWS = WB16 / h16c::WAVES;    // 80 rows per wave
@@ -1304,7 +1330,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
           a = fmaf(cmisc[68 + k], m1[r + k - 3], a);
           a = fmaf(cmisc[75 + k], m2[r + k - 3], a);
         }
-        sa[r] = sigm(a);
+        sa[r] = sigm_fast(a);
       }
     }
   }
@@ -1354,7 +1380,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
       a = fmaf(cmisc[68 + k], m1[r + k - 3], a);
       a = fmaf(cmisc[75 + k], m2[r + k - 3], a);
     }
-    sa[r] = sigm(a);
+    sa[r] = sigm_fast(a);
   }
   __syncthreads();
   st(13);
