@@ -878,6 +878,11 @@ constexpr bool RDN_T16_TAGGED_ON = RDN_T16_TAGGED;
 #ifndef RDN_T16_SA_LOCAL
 #define RDN_T16_SA_LOCAL 0
 #endif
+// RDN_T16_MEAN_MFMA=1: the spatial mean over channels as two MFMAs per row group (A = ca); 0: packed
+// f16 adds and a cross-lane sum
+#ifndef RDN_T16_MEAN_MFMA
+#define RDN_T16_MEAN_MFMA 1
+#endif
 constexpr int EDGE16_WORDS = EDGE16_BYTES / 4;                   // 160 per edge
 #if RDN_T16_TAGGED
 constexpr int SLOT16_BYTES = (G_EDGE + 2 * EDGE16_WORDS) * 8;    // 448 granules = 3584 B
@@ -1348,13 +1353,23 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
 #pragma unroll
     for (int k = 0; k < SROWS / 16; ++k) {
       const V va = ua[k] * cq0, vb = ub[k] * cq4;
-      const V vs = va + vb, vm = __builtin_elementwise_max(va, vb);
+      const V vm = __builtin_elementwise_max(va, vb);
+#if RDN_T16_MEAN_MFMA
+      // sum_c ca_c u_c of row c16 on the idle MFMA pipe: A = ca (every row of the 16 x 32 A-operand
+      // the same, its K order the B-fragment channel order of slots q / q + 4: cq0 / cq4), B = the
+      // two u fragments this lane holds anyway; every output row is the sum, exact f16 products
+      // accumulated in fp32 -- no pk_add tree and no cross-lane sum
+      const f32x4 dsum = h16c::mma(cq4, ub[k], h16c::mma(cq0, ua[k], (f32x4)(0.f)));
+      const float sm = dsum[0];
+#else
+      const V vs = va + vb;
       const h2 s2 = (__builtin_shufflevector(vs, vs, 0, 1) + __builtin_shufflevector(vs, vs, 2, 3)) +
                     (__builtin_shufflevector(vs, vs, 4, 5) + __builtin_shufflevector(vs, vs, 6, 7));
+      const float sm = quarter_sum((float)s2[0] + (float)s2[1]);
+#endif
       const h2 x2 = __builtin_elementwise_max(
           __builtin_elementwise_max(__builtin_shufflevector(vm, vm, 0, 1), __builtin_shufflevector(vm, vm, 2, 3)),
           __builtin_elementwise_max(__builtin_shufflevector(vm, vm, 4, 5), __builtin_shufflevector(vm, vm, 6, 7)));
-      const float sm = quarter_sum((float)s2[0] + (float)s2[1]);
       const float mx = quarter_max(fmaxf((float)x2[0], (float)x2[1]));
       if (ln.q == 0) {
         const int r = SROWS * w + ln.c16 + 16 * k;
