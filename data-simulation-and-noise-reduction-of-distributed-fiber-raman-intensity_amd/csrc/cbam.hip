@@ -1022,7 +1022,7 @@ __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& 
     __builtin_amdgcn_raw_buffer_store_b64(u32x2{m, tag}, sr, 8 * (G_MAX + c), 0, 16);
   } else if (tid < 64 + 2 * EDGE_ROWS * 8) {
     const int i = tid - 64, e = i / (EDGE_ROWS * 8), k = (i / 8) % EDGE_ROWS, g = i & 7;
-    const int r = e == 0 ? 2 * H - EDGE_ROWS + k : T + k;
+    const int r = e == 0 ? WB16 - T - EDGE_ROWS + k : T + k;
     const u32x4 v = *(const u32x4*)(lds + h16c::BUF0 + h16c::soff(r, g));
     const int g0 = G_EDGE + e * EDGE16_WORDS + (k * 8 + g) * 4;
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{v[0], tag, v[1], tag}, sr, 8 * g0, 0, 16);
@@ -1046,7 +1046,7 @@ __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& 
     __hip_atomic_store((unsigned*)(slot + 512) + c, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else if (tid < 64 + 2 * EDGE_ROWS * 8) {
     const int i = tid - 64, e = i / (EDGE_ROWS * 8), k = (i / 8) % EDGE_ROWS, g = i & 7;
-    const int r = e == 0 ? 2 * H - EDGE_ROWS + k : T + k;
+    const int r = e == 0 ? WB16 - T - EDGE_ROWS + k : T + k;
     const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slot, 0, SLOT16_BYTES, 0x00020000);
     const u32x4 v = *(const u32x4*)(lds + h16c::BUF0 + h16c::soff(r, g));
     __builtin_amdgcn_raw_buffer_store_b128(v, sr, STAT_BYTES + e * EDGE16_BYTES + (k * 8 + g) * 16, 0, 16);
@@ -1583,6 +1583,12 @@ static TeamGeo team_geo(int arch, int mode, int64_t L, int dev) {
   g.halo = cb::TEAM_HALO;                  // halos refreshed from the neighbours at every CBAM
   g.T = (p16 ? cb::t16::WB16 : WB) - 2 * g.halo;
   g.TT = (int)((L + g.T - 1) / g.T);
+  // the ping-pong team kernel spreads L evenly over its TT tiles (T = ceil(L / TT) own positions;
+  // the rows beyond them up to the tile's end are its right halo): the last tile then holds few
+  // rows outside [0, L) (9 instead of 54 at L = 10,000), whose zeroing after every conv made it
+  // the slowest member of its team.  RDN_T16_FULL_T=1: every tile owns WB - 2 halo (A/B knob).
+  const char* full = getenv("RDN_T16_FULL_T");
+  if (p16 && !(full && full[0] == '1')) g.T = (int)((L + g.TT - 1) / g.TT);
   const int resident = device_cus(dev) * team_blocks_per_cu(arch, mode, dev);
   g.teams = resident > 0 ? resident / g.TT : 0;
   const char* env = getenv("RDN_CBAM_SEGMENTS");       // diagnostics: force the per-segment path
