@@ -883,6 +883,10 @@ constexpr bool RDN_T16_TAGGED_ON = RDN_T16_TAGGED;
 #ifndef RDN_T16_MEAN_MFMA
 #define RDN_T16_MEAN_MFMA 1
 #endif
+// RDN_T16_SA_PAIR=1: the spatial conv7 two rows per thread, one round
+#ifndef RDN_T16_SA_PAIR
+#define RDN_T16_SA_PAIR 1
+#endif
 constexpr int EDGE16_WORDS = EDGE16_BYTES / 4;                   // 160 per edge
 #if RDN_T16_TAGGED
 constexpr int SLOT16_BYTES = (G_EDGE + 2 * EDGE16_WORDS) * 8;    // 448 granules = 3584 B
@@ -1060,6 +1064,7 @@ __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& 
 
 // apply the CBAM whose statistics sit in the team's slots to u (BUF0): h = [identity +] u*ca*sa
 // [then ReLU], written over u; idv: the identity (LINEAR_SAVE layout) for res != RES_NONE
+template <bool EDGE>
 __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta, const char* slots0, int cbam_slot,
                                         bool bias, int res, const V* idv, Stamps& st, unsigned tag) {
   char* lds = tl.lds;
@@ -1373,7 +1378,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
       const float mx = quarter_max(fmaxf((float)x2[0], (float)x2[1]));
       if (ln.q == 0) {
         const int r = SROWS * w + ln.c16 + 16 * k;
-        const bool in = h16c::in_range(tl.base + r, tl.L);
+        const bool in = !EDGE || h16c::in_range(tl.base + r, tl.L);
         m1[r] = in ? sm * (1.0f / 64.0f) : 0.f;
         m2[r] = in ? mx : 0.f;
       }
@@ -1388,6 +1393,29 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   st(12);
   // sa = sigmoid(conv7([mean_c; max_c]))
   float* sa = (float*)(lds + SA16_OFF);
+#if RDN_T16_SA_PAIR
+  // two adjacent rows per thread (their 7-tap windows share 6 rows): the 320 row pairs of the tile
+  // in one round instead of 640 rows in two
+  for (int i = tid; i < WB16 / 2; i += h16c::THREADS) {
+    const int r = 2 * i;
+    float a0 = bias ? cmisc[82] : 0.f, a1 = a0;
+    float p1[8], p2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      p1[k] = m1[r + k - 3];
+      p2[k] = m2[r + k - 3];
+    }
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      a0 = fmaf(cmisc[68 + k], p1[k], a0);
+      a0 = fmaf(cmisc[75 + k], p2[k], a0);
+      a1 = fmaf(cmisc[68 + k], p1[k + 1], a1);
+      a1 = fmaf(cmisc[75 + k], p2[k + 1], a1);
+    }
+    sa[r] = sigm_fast(a0);
+    sa[r + 1] = sigm_fast(a1);
+  }
+#else
   for (int r = tid; r < WB16; r += h16c::THREADS) {
     float a = bias ? cmisc[82] : 0.f;
 #pragma unroll
@@ -1397,6 +1425,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
     }
     sa[r] = sigm_fast(a);
   }
+#endif
   __syncthreads();
   st(13);
 #endif
@@ -1417,7 +1446,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
       hv += idv[n];
       if (res == RES_ADD_RELU) hv = __builtin_elementwise_max(hv, (V)((_Float16)0));
     }
-    if (!h16c::in_range(tl.base + r, tl.L)) hv = (V)((_Float16)0);
+    if (EDGE && !h16c::in_range(tl.base + r, tl.L)) hv = (V)((_Float16)0);
     *pu = hv;
   }
   __syncthreads();
@@ -1453,7 +1482,7 @@ __device__ __forceinline__ void team16_spectra(char* lds, const uint8_t* blob, c
       team_wait(ta, ctr, (nbar + 1) * (unsigned)ta.TT);
 #endif
       st(4);
-      apply16(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT16_BYTES, slot, ADS, res, id, st, nbar + 1);
+      apply16<EDGE>(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT16_BYTES, slot, ADS, res, id, st, nbar + 1);
       st(5);
       ++nbar;
     };
