@@ -320,6 +320,8 @@ enum Epi : int {
   RES_RELU = 2,   // relu(acc + b + dst)    (DSDN ResidualBlock: out += identity; relu)
   LINEAR_SAVE = 3,  // acc + b, the dst slot's previous content saved to idv[n] first (the CBAM
                     // networks' ResidualBlock identity, held in VGPRs across the CBAM: cbam.hip)
+  STAGE = 4,        // acc + b handed to stg->put(n, v) (VGPRs) instead of stored: the caller writes
+                    // the layer's output after the barrier, in another LDS layout (RDN_F16MIX hybrid)
 };
 
 // LDS byte addresses of this lane's B fragment for k-step s = (tap t, part u) of N-tile n, from
@@ -384,10 +386,14 @@ __device__ __forceinline__ void zero_outside(const Tile& tl, uint32_t dst, int r
   }
 }
 
-template <int EPI, bool EDGE>
+struct NoStage {
+  __device__ void put(int, f32x8) {}
+};
+template <int EPI, bool EDGE, class SG = NoStage>
 __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int dil, const Frags& F, Frags& G,
-                                      bool has_next = true, V* idv = nullptr, ChanStats* cs = nullptr) {
-  static_assert(EPI != LINEAR_SAVE || !RDN_H16_M32, "LINEAR_SAVE: one slot per N-tile");
+                                      bool has_next = true, V* idv = nullptr, ChanStats* cs = nullptr,
+                                      SG* stg = nullptr) {
+  static_assert((EPI != LINEAR_SAVE && EPI != STAGE) || !RDN_H16_M32, "LINEAR_SAVE / STAGE: one slot per N-tile");
   const int lane = tid() & 63, w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB;
   const int next = tl.layer + 1;
   asm volatile("" : "+s"(src), "+s"(dst));   // per-layer addresses: not hoisted out of a network's loop (spills)
@@ -449,6 +455,10 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     // pay the per-lane check and select; the other N-tiles of an edge tile store unmasked
     bool valid = true;
     if constexpr (EDGE && !RDN_H16_EDGE_POST) valid = in_range(pos0 + NR * n + (lane & 15), tl.L);
+    if constexpr (EPI == STAGE) {
+      stg->put(n, __builtin_shufflevector(a.v[0], a.v[1], 0, 1, 2, 3, 4, 5, 6, 7));
+      return;
+    }
     V* p = (V*)(tl.lds + sa + n * NR * ROWB);
     if constexpr (EPI == LINEAR_SAVE) idv[n] = *p;
     const f32x8 v = __builtin_shufflevector(a.v[0], a.v[1], 0, 1, 2, 3, 4, 5, 6, 7);
@@ -494,7 +504,7 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     prev = acc;
   }
   epilogue(NT - 1, prev);
-  if constexpr (EDGE && RDN_H16_EDGE_POST) zero_outside(tl, dst, pos0 - tl.base, h, lane);
+  if constexpr (EDGE && RDN_H16_EDGE_POST && EPI != STAGE) zero_outside(tl, dst, pos0 - tl.base, h, lane);
   tl.layer += 1;
 #if defined(RDN_ABLATE_NOBARRIER)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -24,6 +24,48 @@ __device__ __forceinline__ void pingpong_to_tile(char* lds, uint32_t src) {
   __syncthreads();
 }
 
+// RDN_F16MIX_STAGE=1: the producer of the corrected tail (the layer before it, which writes the e4m3
+// planes) runs on the ping-pong engine with its outputs staged in VGPRs as the in-place tile's three
+// planes and written after the layer's barrier -- no in-place plain layer and no conversion pass;
+// 0: the ping-pong buffer is converted (pingpong_to_tile) and that layer runs on the in-place engine
+#ifndef RDN_F16MIX_STAGE
+#define RDN_F16MIX_STAGE 1
+#endif
+
+// the staged outputs of one ping-pong layer as the in-place H8 row planes: lane (w, q, c16) holds
+// N-tile n's row (w % RB) * RW + 16 n + c16 at 16-B slot 4 (w / RB) + q -- the f16 slot, and the
+// 8-B e4m3 (hi / 4) and e4m3 (lo * 2^9) slots of the same 8 channels (h16_channel order in every
+// plane, inplace.hpp Op<MODE_H8>::sbyte)
+struct H8Stage {
+  f16x8 hi[PPNS::NT];
+  uint32_t e_hi[PPNS::NT][2], e_lo[PPNS::NT][2];
+  __device__ __forceinline__ void put(int n, PPNS::f32x8 v) {
+    const f32x4 a = h8_sat<true>(__builtin_shufflevector(v, v, 0, 1, 2, 3));
+    const f32x4 b = h8_sat<true>(__builtin_shufflevector(v, v, 4, 5, 6, 7));
+    const H8Split sa = h8_split(a), sb = h8_split(b);
+    hi[n] = __builtin_shufflevector(sa.hi, sb.hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    e_hi[n][0] = sa.hi8;
+    e_hi[n][1] = sb.hi8;
+    e_lo[n][0] = sa.lo8;
+    e_lo[n][1] = sb.lo8;
+  }
+  // after the layer's barrier (every read of its input done): rows outside [0, L) as zeros
+  template <bool EDGE>
+  __device__ __forceinline__ void write(char* lds, const PPNS::Tile& t) const {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const int tid = PPNS::tid(), w = tid >> 6, lane = tid & 63;
+    const int g = 4 * (w / PPNS::RB) + (lane >> 4), r0 = (w % PPNS::RB) * PPNS::RW + (lane & 15);
+#pragma unroll
+    for (int n = 0; n < PPNS::NT; ++n) {
+      const int r = r0 + 16 * n;
+      const bool ok = !EDGE || in_range(t.base + r, t.L);
+      *(f16x8*)(lds + off_f32(r, 16 * g)) = ok ? hi[n] : (f16x8)((_Float16)0);
+      *(u32x2*)(lds + off_f32(r, 128 + 8 * g)) = ok ? u32x2{e_hi[n][0], e_hi[n][1]} : u32x2{0u, 0u};
+      *(u32x2*)(lds + off_f32(r, 192 + 8 * g)) = ok ? u32x2{e_lo[n][0], e_lo[n][1]} : u32x2{0u, 0u};
+    }
+  }
+};
+
 template <bool EDGE, int TAIL>
 __device__ __forceinline__ void rrcdnet_hybrid_body(Tile& tl, const uint8_t* blob, const float* x, float* y, int n,
                                                     int L, int T, int tiles) {
@@ -35,6 +77,28 @@ __device__ __forceinline__ void rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   PPNS::load_frags(t16, 0, F0);
   PPNS::stem(t16, 0, PPNS::BUF0);
   PPNS::lds_barrier();
+  f32x4 id[16 * NBK / 4];
+  LayerA<MODE_H8> a;
+#if RDN_F16MIX_STAGE
+  // layers 0 .. PP - 1 plain, layer PP (the tail's producer) staged into the in-place planes
+  for (int i = 0; i < PP / 2; ++i) {
+    PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1);
+    PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF1, PPNS::BUF0, 1, F1, F0);
+  }
+  {
+    H8Stage stg;
+    if constexpr (PP % 2 == 1) {
+      PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1);
+      PPNS::layer<PPNS::STAGE, EDGE>(t16, PPNS::BUF1, PPNS::BUF0, 1, F1, F0, false, nullptr, nullptr, &stg);
+    } else {
+      PPNS::layer<PPNS::STAGE, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1, false, nullptr, nullptr, &stg);
+    }
+    stg.write<EDGE>(tl.lds, t16);
+  }
+  tl.layer = PP + 1;
+  load_layer_a<MODE_H8>(tl, PP + 1, a);
+  __syncthreads();
+#else
   for (int i = 0; i < (PP - 1) / 2; ++i) {
     PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1);
     PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF1, PPNS::BUF0, 1, F1, F0);
@@ -49,12 +113,11 @@ __device__ __forceinline__ void rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
     PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF1, PPNS::BUF0, 1, F1, F0, false);
     cur = PPNS::BUF0;
   }
-  f32x4 id[16 * NBK / 4];
-  LayerA<MODE_H8> a;
   tl.layer = PP;
   load_layer_a<MODE_H8>(tl, PP, a);
   pingpong_to_tile(tl.lds, cur);
   conv<MODE_H8, RELU, 1, EDGE, NBK, false, true, true>(tl, 1, id, a, true);       // writes the e4m3 planes
+#endif
   for (int i = 0; i < TAIL; ++i) conv<MODE_H8, RELU, 1, EDGE, NBK, true, true, true>(tl, 1, id, a, i + 1 < TAIL);
   double r[HO::ROWS];
   head<MODE_H8, NBK>(tl, 2, r);
