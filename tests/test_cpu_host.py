@@ -20,10 +20,9 @@ def test_oracle_reproduces_reference_outputs(arch, inputs):
     from oracle.models import forward
     g = load_golden(arch)
     whichs = ["synth"] + (["trained"] if any(k.startswith("w::") for k in g.files) else [])
-    sets = ["main", "edge7", "edge33"] if arch in ("ADSDN", "APIDN") else INPUT_SETS
     for which in whichs:
         sd = golden_state_dict(arch, which)
-        for name in sets:
+        for name in INPUT_SETS:         # every input set, L = 7 ... 16384, for all six networks
             x = torch.from_numpy(input_array(inputs, name)).unsqueeze(1)
             y = forward(arch, sd, x).squeeze(1).numpy()
             ref = g[f"{which}_{name}"]
