@@ -38,9 +38,18 @@ constexpr int CORR_SLOT = 63;
 // RDN_F16MIX (RRCDNet): the last RDN_F16MIX_TAIL right-branch layers (of 15) keep the e4m3
 // correction (pack.cpp f16mix_default_mask, fused_inplace.hip rrcdnet_hybrid)
 #ifndef RDN_F16MIX_TAIL
-#define RDN_F16MIX_TAIL 3
+#define RDN_F16MIX_TAIL 5
 #endif
 constexpr int F16MIX_TAIL = RDN_F16MIX_TAIL;
+// RDN_F16MIX spiked-tile fallback: a tile whose input window holds a value outside
+// [F16MIX_WIN_LO, F16MIX_WIN_HI] runs every layer corrected (the RDN_F16F8 body on the same blob).
+// The simulator's clean signal is min-max normalised to [0, 1] and its Gaussian noise stays below
+// ~0.05 (SNR >= 20 dB), so only the spikes (5-15 sigma) and the extreme-noise spectra leave the
+// window: 0.17 % of the tiles of config 1's data.  F16MIX_WIN_LO > F16MIX_WIN_HI disables it.
+#ifndef RDN_F16MIX_WIN
+#define RDN_F16MIX_WIN 1
+#endif
+constexpr float F16MIX_WIN_LO = RDN_F16MIX_WIN ? -0.3f : 1.0f, F16MIX_WIN_HI = RDN_F16MIX_WIN ? 1.3f : 0.0f;
 // slot 63 word 2: layout tag BLOB_MAGIC | arch << 8 | dtype, written by rdn_pack for every dtype
 // (include/raman_mi355x.h RDN_BLOB_MAGIC); the RDN_F16MIX kernels check it before reading the blob
 constexpr uint32_t BLOB_MAGIC = 0x52440000u;

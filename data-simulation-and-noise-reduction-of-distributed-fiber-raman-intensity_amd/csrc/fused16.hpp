@@ -283,11 +283,14 @@ __device__ __forceinline__ void mstep(const Frags& F, int s, V b, Acc& acc) {
 // Conv1d(1, 64, 3, padding=1) (+ folded BN) + ReLU in fp32: one (row, 16-B slot) item per lane,
 // 640 x 8 items over the workgroup (the slot is wave-uniform, so the weights are scalar loads).
 // ACCUM adds the result onto the resident row (PIDN/train.py:105, identity recomputed from x).
+// out_lo / out_hi (lo <= hi): returns whether any input this thread read at the tile's rows lies
+// outside [lo, hi] (the RDN_F16MIX spiked-tile test, rrcdnet_hybrid.hpp), else false
 template <bool ACCUM = false>
-__device__ __forceinline__ void stem(const Tile& tl, int sslot, uint32_t dst) {
+__device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, float out_lo = 1.f, float out_hi = 0.f) {
   const float* swp = tl.small + sslot * SMALL_SLOT_FLOATS;
   asm volatile("" : "+s"(swp));      // no reuse of scalar-loaded weights across the layers in between
   const cfloat* sw = (const cfloat*)swp;
+  bool outside = false;
   for (int i = tid(); i < WB * 8; i += THREADS) {
     const int g = __builtin_amdgcn_readfirstlane(i / WB);
     const int row = i - g * WB;
@@ -296,6 +299,7 @@ __device__ __forceinline__ void stem(const Tile& tl, int sslot, uint32_t dst) {
     const float x0 = in_range(p, tl.L) ? tl.x[p] : 0.f;
     const float xp = in_range(p + 1, tl.L) ? tl.x[p + 1] : 0.f;
     const bool valid = in_range(p, tl.L);
+    if (out_lo <= out_hi) outside = outside || x0 < out_lo || x0 > out_hi;
     V* ptr = (V*)(tl.lds + dst + soff(row, g));
     V v;
     if (ACCUM) v = *ptr;
@@ -312,6 +316,7 @@ __device__ __forceinline__ void stem(const Tile& tl, int sslot, uint32_t dst) {
     }
     *ptr = v;
   }
+  return outside;
 }
 
 enum Epi : int {

@@ -218,7 +218,40 @@ __device__ __forceinline__ void nan_outputs(const Tile& tl, float* y, int n, int
   }
 }
 
-// RDN_F16MIX RRCDNet: hybrid bodies on 640-row tiles, the in-place body on short last tiles
+// The all-corrected body of a spiked tile (RDN_F16F8 on the RDN_F16MIX blob, which carries every
+// layer's e4m3 correction fragments)
+template <bool EDGE, int NBK>
+__device__ __forceinline__ void rrcdnet_f16f8_tile(Tile& tl, float* y, int n, int L, int T) {
+  rrcdnet_body<MODE_H8, EDGE, NBK, 0>(tl, y, n, L, T);
+}
+
+// Whether any input of the tile's rows [base, base + WB) inside [0, L) lies outside [lo, hi]
+// (workgroup-uniform; a vote word per wave at the end of the LDS, read before a barrier that precedes
+// any other LDS write)
+__device__ __forceinline__ bool window_outside(const Tile& tl, float lo, float hi) {
+  bool out = false;
+  if (lo <= hi) {
+    for (int r = __builtin_amdgcn_workitem_id_x(); r < TileGeo<5>::WB; r += THREADS) {
+      const int p = tl.base + r;
+      if (in_range(p, tl.L)) {
+        const float v = tl.x[p];
+        out = out || v < lo || v > hi;
+      }
+    }
+  }
+  unsigned* vote = (unsigned*)(tl.lds + TileGeo<5>::LDS) - THREADS / 64;
+  const bool wave_out = __builtin_amdgcn_ballot_w64(out) != 0;
+  if ((__builtin_amdgcn_workitem_id_x() & 63) == 0) vote[__builtin_amdgcn_workitem_id_x() >> 6] = wave_out ? 1u : 0u;
+  __syncthreads();
+  bool any = false;
+#pragma unroll
+  for (int k = 0; k < THREADS / 64; ++k) any = any || vote[k] != 0;
+  __syncthreads();
+  return any;
+}
+
+// RDN_F16MIX RRCDNet: hybrid bodies on 640-row tiles, the in-place body on short last tiles; a tile
+// whose input window leaves [F16MIX_WIN_LO, F16MIX_WIN_HI] (a spike) runs every layer corrected
 template <int TAIL>
 __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restrict__ blob, const float* __restrict__ x,
                                                           float* __restrict__ y, int L, int T, int tiles) {
@@ -227,11 +260,18 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restr
   Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
   if (!f16mix_blob_ok(blob)) return nan_outputs(tl, y, n, T);
   const int need = L - tl.base + 2;
-  if (tl.base >= 0 && tl.base + TileGeo<5>::WB <= L) hyb640::rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles);
-  else if (need <= 256) rrcdnet_body<MODE_H8, true, 2, TAIL>(tl, y, n, L, T);
-  else if (need <= 384) rrcdnet_body<MODE_H8, true, 3, TAIL>(tl, y, n, L, T);
-  else if (need <= 512) rrcdnet_body<MODE_H8, true, 4, TAIL>(tl, y, n, L, T);
-  else hyb640::rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles);
+  if (tl.base >= 0 && tl.base + TileGeo<5>::WB <= L) {
+    if (!hyb640::rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles))
+      rrcdnet_f16f8_tile<false, 5>(tl, y, n, L, T);                // spiked tile: every layer corrected
+  } else if (need <= 512) {
+    // short last tile (the in-place body on the fewest blocks): all layers corrected when spiked
+    const bool spiked = window_outside(tl, F16MIX_WIN_LO, F16MIX_WIN_HI);
+    if (need <= 256) spiked ? rrcdnet_f16f8_tile<true, 2>(tl, y, n, L, T) : rrcdnet_body<MODE_H8, true, 2, TAIL>(tl, y, n, L, T);
+    else if (need <= 384) spiked ? rrcdnet_f16f8_tile<true, 3>(tl, y, n, L, T) : rrcdnet_body<MODE_H8, true, 3, TAIL>(tl, y, n, L, T);
+    else spiked ? rrcdnet_f16f8_tile<true, 4>(tl, y, n, L, T) : rrcdnet_body<MODE_H8, true, 4, TAIL>(tl, y, n, L, T);
+  } else if (!hyb640::rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles)) {
+    rrcdnet_f16f8_tile<true, 5>(tl, y, n, L, T);
+  }
 }
 
 // RDN_F16MIX RRCDNet on 256-row tiles (the hybrid body on h16xs + the 2-block in-place tile): the
@@ -243,8 +283,11 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_short(const uint8_t* __restri
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
   if (!f16mix_blob_ok(blob)) return nan_outputs(tl, y, n, T);
-  if (tl.base >= 0 && tl.base + TileGeo<2>::WB <= L) hyb256::rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles);
-  else hyb256::rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles);
+  if (tl.base >= 0 && tl.base + TileGeo<2>::WB <= L) {
+    if (!hyb256::rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles)) rrcdnet_f16f8_tile<false, 2>(tl, y, n, L, T);
+  } else if (!hyb256::rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles)) {
+    rrcdnet_f16f8_tile<true, 2>(tl, y, n, L, T);
+  }
 }
 
 #define IP_KERNEL(name, arch)                                                                              \

@@ -66,8 +66,10 @@ struct H8Stage {
   }
 };
 
+// Returns false, having written nothing, when the tile's input window leaves [F16MIX_WIN_LO,
+// F16MIX_WIN_HI] (common.hpp): the caller then runs the all-corrected body on the tile.
 template <bool EDGE, int TAIL>
-__device__ __forceinline__ void rrcdnet_hybrid_body(Tile& tl, const uint8_t* blob, const float* x, float* y, int n,
+__device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blob, const float* x, float* y, int n,
                                                     int L, int T, int tiles) {
   constexpr int H = fused_halo(RRCDNET), NBK = HNBK, PP = 14 - TAIL;   // ping-pong layers of the right branch
   using HO = HeadOut<MODE_H8, NBK>;
@@ -75,8 +77,22 @@ __device__ __forceinline__ void rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   PPNS::Tile t16 = PPNS::make_tile(tl.lds, blob, x, L, T, tiles, H, n16);
   PPNS::Frags F0, F1;            // alternating operand buffers (fused16.hpp layer)
   PPNS::load_frags(t16, 0, F0);
-  PPNS::stem(t16, 0, PPNS::BUF0);
-  PPNS::lds_barrier();
+  {
+    // the stem tests its inputs against the window; one word per wave at the end of the LDS (first
+    // written by layer 0, after the barrier below and the read behind it)
+    const bool out = PPNS::stem(t16, 0, PPNS::BUF0, F16MIX_WIN_LO, F16MIX_WIN_HI);
+    unsigned* vote = (unsigned*)(tl.lds + PPNS::LDS_BYTES) - PPNS::WAVES;
+    const bool wave_out = __builtin_amdgcn_ballot_w64(out) != 0;
+    if ((PPNS::tid() & 63) == 0) vote[PPNS::tid() >> 6] = wave_out ? 1u : 0u;
+    PPNS::lds_barrier();
+    bool spiked = false;
+#pragma unroll
+    for (int k = 0; k < PPNS::WAVES; ++k) spiked = spiked || vote[k] != 0;
+    if (spiked) {
+      __syncthreads();             // every wave has read the votes before the fallback body writes
+      return false;
+    }
+  }
   f32x4 id[16 * NBK / 4];
   LayerA<MODE_H8> a;
 #if RDN_F16MIX_STAGE
@@ -155,5 +171,6 @@ __device__ __forceinline__ void rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
     o[k] = (float)((double)xv - (parked_row<MODE_H8, NBK>(tl, y, n, k, H, T) + (double)lrow[HO::row(k)]) * 0.5);
   }
   store_out<MODE_H8, NBK>(tl, y, n, o, H, T);
+  return true;
 }
 

@@ -89,7 +89,7 @@ def test_blob_layout_tag(lib):
     bm = engine.pack("RRCDNet", sd, "f16mix", "cpu")
     engine.check_blob("RRCDNet", "f16f8", b8)
     engine.check_blob("RRCDNet", "f16", bm)
-    assert engine.correction_mask("RRCDNet", "f16", bm) == 0x7 << 12
+    assert engine.correction_mask("RRCDNet", "f16", bm) == 0x1f << 10
     with pytest.raises(_lib.EngineError, match="needs"):
         engine.check_blob("RRCDNet", "f16mix", b8)                 # too small for the F16MIX layout
     padded = torch.cat([b8, torch.zeros(bm.numel() - b8.numel(), dtype=torch.uint8)])
@@ -414,12 +414,12 @@ def test_host_sanitizer_pack(arch, dtype, tmp_path):
 
 def test_correction_masks_recorded_in_blob():
     """RDN_F16F8 blobs record every layer as corrected, RDN_F16MIX (RRCDNet only) the compiled-in tail
-    right_net.15-17 = big layers 12-14; the other networks refuse RDN_F16MIX."""
+    right_net.13-17 = big layers 10-14; the other networks refuse RDN_F16MIX."""
     from raman_mi355x import engine, _lib
     sd = golden_state_dict("RRCDNet", "trained")
     assert engine.correction_mask("RRCDNet", "f16f8", engine.pack("RRCDNet", sd, "f16f8", "cpu")) == (1 << 64) - 1
-    assert engine.correction_mask("RRCDNet", "f16mix", engine.pack("RRCDNet", sd, "f16mix", "cpu")) == 0x7 << 12
-    assert engine.default_correction_mask("RRCDNet") == 0x7 << 12
+    assert engine.correction_mask("RRCDNet", "f16mix", engine.pack("RRCDNet", sd, "f16mix", "cpu")) == 0x1f << 10
+    assert engine.default_correction_mask("RRCDNet") == 0x1f << 10
     for arch in ("DenoiseCNN", "DSDN", "PIDN", "ADSDN", "APIDN"):
         assert engine.default_correction_mask(arch) == 0
         with pytest.raises(_lib.EngineError, match="RRCDNet"):

@@ -302,3 +302,52 @@ def test_f16_resolves_per_network():
         m = R.MODELS[arch]().set_engine_dtype("f16")
         assert m.engine_code == (engine.F16MIX if arch == "RRCDNet" else engine.F16), arch
     assert R.RRCDNet().set_engine_dtype("f16-plain").engine_code == engine.F16
+
+
+# --- RDN_F16MIX spiked-tile fallback (common.hpp F16MIX_WIN_*) --------------------------------------
+def _config1_spectra(idx):
+    """Spectra `idx` of config 1's data/test.npz (1000 spectra of the reference generator at seed
+    20250410, oracle.refgen: bit-exact with 数据集产生.py), float32 like the saved npz."""
+    from oracle.refgen import generate_signals
+    rng = np.random.RandomState(20250410)
+    _, noisy, _, _ = generate_signals(1000, rng=rng)
+    return np.ascontiguousarray(noisy[idx].astype(np.float32))
+
+
+@pytest.mark.parametrize("short", ["0", "1"])
+def test_f16mix_config1_worst_spectra_within_bar(short, monkeypatch):
+    """'f16' on RRCDNet (trained fixture weights) over the spectra of config 1's data that came closest
+    to the bar before the spiked-tile fallback and the 5-layer tail (profiles/r03/ablate/
+    f16mix_window_eval.log: 373 and 795 -- spikes -- were 2.2e-2, 26 and 888 1.96e-2 / 1.8e-2), plus two
+    ordinary ones; both tile geometries (RDN_SHORT_TILES)."""
+    from oracle.models import forward as oracle_forward
+    monkeypatch.setenv("RDN_SHORT_TILES", short)
+    idx = [373, 795, 26, 888, 368, 0]
+    x = _config1_spectra(idx)
+    sd = golden_state_dict("RRCDNet", "trained")
+    ref = oracle_forward("RRCDNet", sd, torch.from_numpy(x).unsqueeze(1)).squeeze(1).numpy()
+    y = _run(_model("RRCDNet", "trained", "f16"), x)
+    err = np.abs(y - ref).max(axis=1)
+    print("config-1 spectra", idx, "f16 max-abs", [f"{e:.3e}" for e in err])
+    assert err.max() <= BF16_ABS, err
+
+
+def test_f16mix_spiked_tile_runs_all_corrected():
+    """A tile whose input window leaves [-0.3, 1.3] runs every layer corrected: its own positions equal
+    the RDN_F16F8 forward bit for bit (same in-place body, same 640-row tile geometry), while the other
+    tiles run the hybrid (different bits, both within the bar)."""
+    monkey = pytest.MonkeyPatch()
+    monkey.setenv("RDN_SHORT_TILES", "0")
+    try:
+        x = _config1_spectra([0, 1])
+        T, H = 582, 29
+        x[0, 5 * T + 100] = 3.0                      # a spike in tile 5 of spectrum 0 (its window only)
+        y16 = _run(_model("RRCDNet", "trained", "f16"), x)
+        y8 = _run(_model("RRCDNet", "trained", "f16f8"), x)
+    finally:
+        monkey.undo()
+    # tile 5 owns [5T, 6T); the spike at 5T + 100 also lies in tile 4's window [4T - H, 5T + H)? no:
+    # 5T + 100 >= 5T + H, so only tile 5's window [5T - H, 6T + H) holds it
+    assert np.array_equal(y16[0, 5 * T:6 * T], y8[0, 5 * T:6 * T])
+    assert not np.array_equal(y16[0, 4 * T:5 * T], y8[0, 4 * T:5 * T])
+    assert not np.array_equal(y16[1], y8[1])
