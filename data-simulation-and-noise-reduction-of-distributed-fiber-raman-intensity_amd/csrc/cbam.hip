@@ -887,6 +887,10 @@ constexpr bool RDN_T16_TAGGED_ON = RDN_T16_TAGGED;
 #ifndef RDN_T16_SA_PAIR
 #define RDN_T16_SA_PAIR 1
 #endif
+// RDN_T16_MLP_BFLY=1: the channel-attention MLP's 8 hidden sums by one lane butterfly
+#ifndef RDN_T16_MLP_BFLY
+#define RDN_T16_MLP_BFLY 1
+#endif
 constexpr int EDGE16_WORDS = EDGE16_BYTES / 4;                   // 160 per edge
 #if RDN_T16_TAGGED
 constexpr int SLOT16_BYTES = (G_EDGE + 2 * EDGE16_WORDS) * 8;    // 448 granules = 3584 B
@@ -1256,6 +1260,39 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
       m = max(m, pm[k * 64 + lane]);
     }
     const float pa = (float)sum * __builtin_amdgcn_rcpf((float)tl.L), px = ord2f(m);
+#if RDN_T16_MLP_BFLY
+    // the 8 hidden sums (fc.0 row j of the pooled avg / max, over the 64 lanes = channels) by one
+    // butterfly instead of 8 separate reductions: lane halves swap (avg | max), then lane quarters
+    // (j pairs), rows of 8 (ror 8), and 3 DPP adds finish each 8-lane group; lane 8g of the wave then
+    // holds hidden sum (avg if g < 4 else max, j = {0, 2, 1, 3}[g & 3])
+    float t[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(w1v[j] * pa), __float_as_uint(w1v[j] * px), false, false);
+      t[j] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    }
+    float u[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(t[2 * k]), __float_as_uint(t[2 * k + 1]), false, false);
+      u[k] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    }
+    const bool hi8 = (lane & 8) != 0;
+    float r = (hi8 ? u[1] : u[0]) + dpp<0x128>(hi8 ? u[0] : u[1]);     // row_ror:8
+    r += dpp<0xB1>(r);
+    r += dpp<0x4E>(r);
+    r += dpp<0x141>(r);
+    float oa = 2.f * b2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int g = j == 0 ? 0 : j == 1 ? 2 : j == 2 ? 1 : 3;          // lane group of hidden unit j
+      const float b1 = bias ? cmisc[j] : 0.f;
+      const float ha = fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 8 * g)) + b1, 0.f);
+      const float hm = fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 32 + 8 * g)) + b1, 0.f);
+      oa = fmaf(cw2v[j], ha + hm, oa);
+    }
+    cav = sigm_fast(oa);
+#else
     float oa = b2, om = b2;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1266,6 +1303,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
       om = fmaf(cw2v[j], hm, om);
     }
     cav = sigm_fast(oa + om);
+#endif
   }
   // this lane's 8 channels of ca through the wave's own LDS row (in-order within a wave)
   float* caw = (float*)(lds + CA16_OFF) + 64 * w;
