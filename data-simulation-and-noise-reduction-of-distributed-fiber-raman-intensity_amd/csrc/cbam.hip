@@ -891,6 +891,9 @@ constexpr bool RDN_T16_TAGGED_ON = RDN_T16_TAGGED;
 #ifndef RDN_T16_MLP_BFLY
 #define RDN_T16_MLP_BFLY 1
 #endif
+#ifndef RDN_T16_POLL_PER
+#define RDN_T16_POLL_PER 4
+#endif
 constexpr int EDGE16_WORDS = EDGE16_BYTES / 4;                   // 160 per edge
 #if RDN_T16_TAGGED
 constexpr int SLOT16_BYTES = (G_EDGE + 2 * EDGE16_WORDS) * 8;    // 448 granules = 3584 B
@@ -1103,7 +1106,9 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   bool edge_ok = eoff < 0;
   {
     const int c = tid & 63, part = tid >> 6;
-    constexpr int PER = 2, STEP = h16c::WAVES * PER;
+    // slots per thread per poll batch: 4 -> one batch (one round trip) for up to 32 tiles, i.e. up to
+    // L = 20,096 (L = 16,384: 27 tiles; 2 per thread made that two batches polled one after the other)
+    constexpr int PER = RDN_T16_POLL_PER, STEP = h16c::WAVES * PER;
     const int nbatch = (ta.TT + STEP - 1) / STEP;
     // this tile's own slot is not polled: its granules are the values publish16 stored, recomputed
     // from the same LDS partials in the same order (same bits), so the last tile to publish goes on
