@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--sel", type=int, default=64)
     ap.add_argument("--masks", nargs="*", default=["tail3", "tail4", "tail5", "tail6", "tail7"])
     ap.add_argument("--extra", nargs="*", default=[], help="extra masks as comma lists of big-layer indices")
+    ap.add_argument("--windows", nargs="*", default=["-0.3,1.3", "-0.5,1.5"], help="fallback windows lo,hi")
     args = ap.parse_args()
     from oracle.models import forward as oracle_forward
     from oracle.refgen import generate_signals
@@ -82,14 +83,17 @@ def main():
             y = emulate(sd, xs, cm)
             e = np.abs(y - rs)
             line = [f"  {name:24s} worst-{args.sel}: max {e.max():.4e}"]
-            for lo, hi in ((-0.3, 1.3), (-0.5, 1.5)):
+            for win in args.windows:
+                lo, hi = (float(v) for v in win.strip("[]").split(","))
                 comp = e.copy()
+                nfall = 0
                 for t in range(tiles):
                     a0, b0 = max(0, t * T - H), min(L, t * T - H + 640)
                     fall = (x[sel, a0:b0].max(axis=1) > hi) | (x[sel, a0:b0].min(axis=1) < lo)
                     a, b = t * T, min(L, (t + 1) * T)
                     comp[fall, a:b] = np.abs(full - rs)[fall, a:b]
-                line.append(f"+fallback[{lo},{hi}] {comp.max():.4e}")
+                    nfall += int(fall.sum())
+                line.append(f"+fallback[{lo},{hi}] {comp.max():.4e} ({nfall} of {len(sel) * tiles} tiles)")
             print("  ".join(line), flush=True)
 
 
