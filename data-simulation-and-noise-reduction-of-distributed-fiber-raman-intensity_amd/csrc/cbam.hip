@@ -329,6 +329,7 @@ struct TeamArgs {
   unsigned* err;         // hand-off error words: [0] this launch (fast-fail, NaN outputs), [1] sticky (cbam_status)
   unsigned long long* stamps;   // RDN_TEAM_STAMPS diagnostics: [grid][NSTAMP] cycle sums per phase
   int force_miss;       // test knob (RDN_CBAM_FORCE_MISS=k): workgroup 0 skips its k-th arrival
+  int xcd;              // team16: 1 = same-XCD teams may hand off through their XCD's L2 (RDN_T16_XCD)
 };
 #ifndef RDN_TEAM_STAMPS
 #define RDN_TEAM_STAMPS 0
@@ -894,6 +895,13 @@ constexpr bool RDN_T16_TAGGED_ON = RDN_T16_TAGGED;
 #ifndef RDN_T16_POLL_PER
 #define RDN_T16_POLL_PER 4
 #endif
+// RDN_T16_XCD=1: teams placed on one XCD each (see team16_forward) hand off through that XCD's L2
+// (plain slot stores) once the launch's first CBAM has confirmed the placement
+#ifndef RDN_T16_XCD
+#define RDN_T16_XCD 1
+#endif
+// s_getreg operand of HW_REG_XCC_ID (id 20), bits [3:0]
+constexpr int HWREG_XCC_ID = (3 << 11) | 20;
 constexpr int EDGE16_WORDS = EDGE16_BYTES / 4;                   // 160 per edge
 #if RDN_T16_TAGGED
 constexpr int SLOT16_BYTES = (G_EDGE + 2 * EDGE16_WORDS) * 8;    // 448 granules = 3584 B
@@ -968,8 +976,23 @@ __device__ __forceinline__ float quarter_max(float v) {
 
 // per-channel sum / max of u (BUF0) over the tile's own positions and its edge rows -> slot (sc1);
 // arrive at the team counter
+typedef unsigned int gu32x2 __attribute__((ext_vector_type(2)));
+template <int AUX>
+__device__ __forceinline__ void slot_store64(gu32x2 v, __amdgpu_buffer_rsrc_t sr, int off) {
+  __builtin_amdgcn_raw_buffer_store_b64(v, sr, off, 0, AUX);
+}
+template <int AUX>
+__device__ __forceinline__ void slot_store128(u32x4 v, __amdgpu_buffer_rsrc_t sr, int off) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, sr, off, 0, AUX);
+}
+// xmode (RDN_T16_XCD): XM_PROBE = the launch's first CBAM (sc1 stores; every sum granule's tag carries
+// bit 31 when this tile cannot hand off through its XCD's L2), XM_L2 = plain stores (the line stays
+// in the team's one L2, which every member's L1-bypassing loads read), XM_SC1 = sc1 stores
+enum XMode : int { XM_PROBE = 0, XM_L2 = 1, XM_SC1 = 2 };
+constexpr unsigned TAG_OFF_XCD = 0x80000000u;
 __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& ta, char* slot, unsigned* ctr,
-                                          bool arrive, const h16c::ChanStats* pre, unsigned tag) {
+                                          bool arrive, const h16c::ChanStats* pre, unsigned tag, int xmode,
+                                          bool local) {
   char* lds = tl.lds;
   const Lane ln;
   const int tid = h16c::tid();
@@ -1028,16 +1051,26 @@ __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& 
       sv += (double)rs[k * 64 + c];
       m = max(m, rm[k * 64 + c]);
     }
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint((float)sv), tag}, sr, 8 * (G_SUM + c), 0, 16);
-    __builtin_amdgcn_raw_buffer_store_b64(u32x2{m, tag}, sr, 8 * (G_MAX + c), 0, 16);
+    const unsigned tsum = xmode == XM_PROBE && !local ? tag | TAG_OFF_XCD : tag;
+    if (xmode == XM_L2) {
+      slot_store64<0>(gu32x2{__float_as_uint((float)sv), tsum}, sr, 8 * (G_SUM + c));
+      slot_store64<0>(gu32x2{m, tag}, sr, 8 * (G_MAX + c));
+    } else {
+      slot_store64<16>(gu32x2{__float_as_uint((float)sv), tsum}, sr, 8 * (G_SUM + c));
+      slot_store64<16>(gu32x2{m, tag}, sr, 8 * (G_MAX + c));
+    }
   } else if (tid < 64 + 2 * EDGE_ROWS * 8) {
     const int i = tid - 64, e = i / (EDGE_ROWS * 8), k = (i / 8) % EDGE_ROWS, g = i & 7;
     const int r = e == 0 ? WB16 - T - EDGE_ROWS + k : T + k;
     const u32x4 v = *(const u32x4*)(lds + h16c::BUF0 + h16c::soff(r, g));
     const int g0 = G_EDGE + e * EDGE16_WORDS + (k * 8 + g) * 4;
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v[0], tag, v[1], tag}, sr, 8 * g0, 0, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v[2], tag, v[3], tag}, sr, 8 * g0 + 16, 0, 16);
+    if (xmode == XM_L2) {
+      slot_store128<0>(u32x4{v[0], tag, v[1], tag}, sr, 8 * g0);
+      slot_store128<0>(u32x4{v[2], tag, v[3], tag}, sr, 8 * g0 + 16);
+    } else {
+      slot_store128<16>(u32x4{v[0], tag, v[1], tag}, sr, 8 * g0);
+      slot_store128<16>(u32x4{v[2], tag, v[3], tag}, sr, 8 * g0 + 16);
+    }
   }
   (void)ctr;
 #else
@@ -1066,6 +1099,8 @@ __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& 
   __syncthreads();
   if (tid == 0 && arrive) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   (void)tag;
+  (void)xmode;
+  (void)local;
 #endif
 }
 
@@ -1073,7 +1108,8 @@ __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& 
 // [then ReLU], written over u; idv: the identity (LINEAR_SAVE layout) for res != RES_NONE
 template <bool EDGE>
 __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta, const char* slots0, int cbam_slot,
-                                        bool bias, int res, const V* idv, Stamps& st, unsigned tag) {
+                                        bool bias, int res, const V* idv, Stamps& st, unsigned tag, int& xmode,
+                                        bool local) {
   char* lds = tl.lds;
   const Lane ln;
   const int tid = h16c::tid(), lane = tid & 63, w = ln.w;
@@ -1116,7 +1152,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
     const int own = (tl.base + ta.halo) / ta.T;
     double sp = 0.0;
     unsigned mp = 0;
-    bool failed = false;
+    bool failed = false, off_xcd = false;
     unsigned vparity = 0;
     for (int b = 0; b < nbatch; ++b) {
       u32x2 sv[PER], mv[PER];
@@ -1155,7 +1191,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
         bool mine = true;
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
-          ok[k] = ok[k] || (sv[k][1] == tag && mv[k][1] == tag);
+          ok[k] = ok[k] || ((sv[k][1] & ~TAG_OFF_XCD) == tag && mv[k][1] == tag);
           mine = mine && ok[k];
         }
         if (b == 0) {
@@ -1185,6 +1221,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
         if (part + STEP * b + h16c::WAVES * k < ta.TT) {
           sp += (double)__uint_as_float(sv[k][0]);
           mp = max(mp, mv[k][0]);
+          off_xcd = off_xcd || (sv[k][1] & TAG_OFF_XCD) != 0;
         }
       }
     }
@@ -1192,6 +1229,9 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
     unsigned* pm = (unsigned*)(lds + SLP_OFF + 8 * 64 * 8);
     ps[part * 64 + c] = sp;
     pm[part * 64 + c] = mp;
+    // the launch's first CBAM: every member has now seen every member's placement bit (its own:
+    // `local`), so the whole team takes the same decision
+    if (xmode == XM_PROBE) xmode = wg_all(lds, local && !off_xcd && !failed, vparity) ? XM_L2 : XM_SC1;
   }
   if (eoff >= 0) {
     const int r = edge_e == 0 ? edge_k : WB16 - EDGE_ROWS + edge_k;
@@ -1497,8 +1537,10 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
 
 template <bool ADS, bool EDGE>
 __device__ __forceinline__ void team16_spectra(char* lds, const uint8_t* blob, const uint8_t* big16, const float* x,
-                                               float* y, int L, const TeamArgs& ta, int team, int tile) {
+                                               float* y, int L, const TeamArgs& ta, int team, int tile,
+                                               bool local) {
   unsigned* ctr = ta.counters + (size_t)team * TEAM_CTR_STRIDE;
+  int xmode = RDN_T16_TAGGED && RDN_T16_XCD && ta.xcd ? XM_PROBE : XM_SC1;
   char* tslots = ta.slots + (size_t)team * 2 * ta.TT * SLOT16_BYTES;
   unsigned nbar = 0;
   Stamps st;
@@ -1519,13 +1561,14 @@ __device__ __forceinline__ void team16_spectra(char* lds, const uint8_t* blob, c
       char* mine = tslots + ((size_t)(nbar & 1) * ta.TT + tile) * SLOT16_BYTES;
       const bool skip = ta.force_miss > 0 && __builtin_amdgcn_workgroup_id_x() == 0 && nbar + 1 == (unsigned)ta.force_miss;
       st(1);
-      publish16(tl, ta, mine, ctr, !skip, pre, nbar + 1);
+      publish16(tl, ta, mine, ctr, !skip, pre, nbar + 1, xmode, local);
       st(3);
 #if !RDN_T16_TAGGED
       team_wait(ta, ctr, (nbar + 1) * (unsigned)ta.TT);
 #endif
       st(4);
-      apply16<EDGE>(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT16_BYTES, slot, ADS, res, id, st, nbar + 1);
+      apply16<EDGE>(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT16_BYTES, slot, ADS, res, id, st, nbar + 1,
+                    xmode, local);
       st(5);
       ++nbar;
     };
@@ -1578,15 +1621,33 @@ __global__ __launch_bounds__(h16c::THREADS) void team16_forward(const uint8_t* _
                                                                 const float* __restrict__ x, float* __restrict__ y,
                                                                 int L, TeamArgs ta) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int team = __builtin_amdgcn_workgroup_id_x() / ta.TT, tile = __builtin_amdgcn_workgroup_id_x() - team * ta.TT;
+  const int wg = __builtin_amdgcn_workgroup_id_x();
+  int team = wg / ta.TT, tile = wg - team * ta.TT;
+  bool local = false;
+#if RDN_T16_XCD
+  // XCD-aware teams: workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md), so
+  // workgroups 8r + x, r < R0, sit on XCD x; they form teams 8j + x of TT tiles (r = j TT + tile),
+  // each on one XCD, and the workgroups from 8 R0 on form the remaining teams in order.  A member
+  // whose XCC_ID is not x reports it at the first CBAM and its team hands off through sc1 instead.
+  const int tpx = (ta.teams * ta.TT / 8) / ta.TT, R0 = tpx * ta.TT;
+  if (wg < 8 * R0) {
+    const int xc = wg & 7, r = wg >> 3;
+    team = (r / ta.TT) * 8 + xc;
+    tile = r % ta.TT;
+    local = (__builtin_amdgcn_s_getreg(t16::HWREG_XCC_ID) & 0xf) == (unsigned)xc;
+  } else {
+    team = 8 * tpx + (wg - 8 * R0) / ta.TT;
+    tile = (wg - 8 * R0) % ta.TT;
+  }
+#endif
   const int base = tile * ta.T - ta.halo;
   // a tile holds positions outside [0, L) for every spectrum or for none (one L per launch)
 #if defined(RDN_ABLATE_ALLEDGE)          // diagnostic: every tile on the edge-tile code
-  if (false) t16::team16_spectra<ADS, false>(lds, blob, big16, x, y, L, ta, team, tile);
+  if (false) t16::team16_spectra<ADS, false>(lds, blob, big16, x, y, L, ta, team, tile, local);
 #else
-  if (base >= 0 && base + t16::WB16 <= L) t16::team16_spectra<ADS, false>(lds, blob, big16, x, y, L, ta, team, tile);
+  if (base >= 0 && base + t16::WB16 <= L) t16::team16_spectra<ADS, false>(lds, blob, big16, x, y, L, ta, team, tile, local);
 #endif
-  else t16::team16_spectra<ADS, true>(lds, blob, big16, x, y, L, ta, team, tile);
+  else t16::team16_spectra<ADS, true>(lds, blob, big16, x, y, L, ta, team, tile, local);
 }
 
 }  // namespace cb
@@ -1707,6 +1768,8 @@ static hipError_t launch_team(int arch, int mode, const TeamGeo& g, const uint8_
   ta.err = team_err(g, ws);
   const char* miss = getenv("RDN_CBAM_FORCE_MISS");     // test knob: see TeamArgs::force_miss
   ta.force_miss = miss ? atoi(miss) : 0;
+  const char* xcd = getenv("RDN_T16_XCD_OFF");          // A/B knob: every team hands off through sc1
+  ta.xcd = xcd && xcd[0] == '1' ? 0 : 1;
   ta.stamps = cb::STAMP_BYTES ? (unsigned long long*)((char*)ws + g.total - cb::STAMP_BYTES) : nullptr;
   // counters and this launch's error word start at 0 (the hand-off counts arrivals monotonically);
   // the sticky word after it collects every launch's timeouts until cbam_status reads and clears it

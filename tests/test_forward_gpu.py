@@ -216,6 +216,24 @@ def test_cbam_team_timeout_is_reported(arch, dtype, monkeypatch):
     assert torch.isfinite(y).all()
 
 
+@pytest.mark.parametrize("L", [10000, 16384])
+@pytest.mark.parametrize("arch", ["ADSDN", "APIDN"])
+def test_cbam_team16_xcd_handoff_bitwise(arch, L, monkeypatch):
+    """RDN_F16 team kernel: teams placed on one XCD hand off through that XCD's L2 (plain slot stores,
+    cbam.hip RDN_T16_XCD) after the first CBAM has confirmed the placement; every other team, and every
+    team with RDN_T16_XCD_OFF=1, through sc1.  Same values in the same order: bitwise equal outputs,
+    with every team busy (40 spectra; L = 16,384: 8 one-XCD teams + 1 spread team)."""
+    m = _model(arch, "trained", "f16")
+    x = np.random.default_rng(11).uniform(0, 1, (40, L)).astype(np.float32)
+    x[::7, 1000:1040] += 3.0                                 # a few spikes
+    y_xcd = _run(m, x)
+    monkeypatch.setenv("RDN_T16_XCD_OFF", "1")
+    y_sc1 = _run(m, x)
+    monkeypatch.delenv("RDN_T16_XCD_OFF")
+    assert np.isfinite(y_xcd).all()
+    assert np.array_equal(y_xcd, y_sc1)
+
+
 @pytest.mark.parametrize("arch", ["ADSDN", "APIDN"])
 def test_cbam_team_matches_segment_path(arch, monkeypatch):
     """The team-persistent kernel (halo exchange) and the per-segment launches (RDN_CBAM_SEGMENTS=1,

@@ -8,7 +8,7 @@ accumulation; corrected layers from fp32 operands; right head split, left head f
 hybrid), run on the SEL worst spectra of the shipped mask per weight set, plus a per-tile 'spike
 fallback' (tiles whose input window leaves [lo, hi] computed by f16f8, i.e. every layer corrected).
 
-    python tools/f16mix_config1_emul.py [--sel 64] [--masks tail3 tail4 ...]
+    python tools/f16mix_config1_emul.py [--sel 64] [--masks tail3 tail4 ...] [--term both|x|w]
 """
 import argparse
 import os
@@ -34,10 +34,10 @@ def tail(k):
     return set(range(15 - k, 15))
 
 
-def emulate(sd, x, corrected):
+def emulate(sd, x, corrected, term="both"):
     out = []
     for i in range(0, x.shape[0], 16):
-        out.append(rrcdnet(sd, x[i:i + 16].unsqueeze(1), corrected, HEAD).squeeze(1).numpy())
+        out.append(rrcdnet(sd, x[i:i + 16].unsqueeze(1), corrected, HEAD, term).squeeze(1).numpy())
     return np.concatenate(out)
 
 
@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--sel", type=int, default=64)
     ap.add_argument("--masks", nargs="*", default=["tail3", "tail4", "tail5", "tail6", "tail7"])
     ap.add_argument("--extra", nargs="*", default=[], help="extra masks as comma lists of big-layer indices")
+    ap.add_argument("--term", default="both", choices=["both", "x", "w"],
+                    help="correction terms of the masks' layers: both, activation residue only, weight residue only")
     ap.add_argument("--windows", nargs="*", default=["-0.3,1.3", "-0.5,1.5"], help="fallback windows lo,hi")
     args = ap.parse_args()
     from oracle.models import forward as oracle_forward
@@ -80,9 +82,9 @@ def main():
         xs, rs = X[sel], ref[sel]
         full = emulate(sd, xs, set(range(29)))           # f16f8-like: every layer corrected
         for name, cm in masks.items():
-            y = emulate(sd, xs, cm)
+            y = emulate(sd, xs, cm, args.term)
             e = np.abs(y - rs)
-            line = [f"  {name:24s} worst-{args.sel}: max {e.max():.4e}"]
+            line = [f"  {name + '/' + args.term:24s} worst-{args.sel}: max {e.max():.4e}"]
             for win in args.windows:
                 lo, hi = (float(v) for v in win.strip("[]").split(","))
                 comp = e.copy()
