@@ -15,6 +15,7 @@
 //             sum (fp64) and max of u over the tile's own positions for the next CBAM; or, for
 //             the last segment, runs the head (ADSDN: conv_out; APIDN: sigmoid(conv_out(h + h0))).
 // Intermediates live in HBM as fp32 [n][L][64] (256 B per position).
+#include <atomic>
 #include <cstdlib>
 #include <vector>
 
@@ -330,6 +331,7 @@ struct TeamArgs {
   unsigned long long* stamps;   // RDN_TEAM_STAMPS diagnostics: [grid][NSTAMP] cycle sums per phase
   int force_miss;       // test knob (RDN_CBAM_FORCE_MISS=k): workgroup 0 skips its k-th arrival
   int xcd;              // team16: 1 = same-XCD teams may hand off through their XCD's L2 (RDN_T16_XCD)
+  unsigned tag0;        // team16: this launch's first granule tag - 1 (tags never repeat across launches)
 };
 #ifndef RDN_TEAM_STAMPS
 #define RDN_TEAM_STAMPS 0
@@ -1561,14 +1563,14 @@ __device__ __forceinline__ void team16_spectra(char* lds, const uint8_t* blob, c
       char* mine = tslots + ((size_t)(nbar & 1) * ta.TT + tile) * SLOT16_BYTES;
       const bool skip = ta.force_miss > 0 && __builtin_amdgcn_workgroup_id_x() == 0 && nbar + 1 == (unsigned)ta.force_miss;
       st(1);
-      publish16(tl, ta, mine, ctr, !skip, pre, nbar + 1, xmode, local);
+      publish16(tl, ta, mine, ctr, !skip, pre, ta.tag0 + nbar + 1, xmode, local);
       st(3);
 #if !RDN_T16_TAGGED
       team_wait(ta, ctr, (nbar + 1) * (unsigned)ta.TT);
 #endif
       st(4);
-      apply16<EDGE>(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT16_BYTES, slot, ADS, res, id, st, nbar + 1,
-                    xmode, local);
+      apply16<EDGE>(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT16_BYTES, slot, ADS, res, id, st,
+                    ta.tag0 + nbar + 1, xmode, local);
       st(5);
       ++nbar;
     };
@@ -1775,12 +1777,25 @@ static hipError_t launch_team(int arch, int mode, const TeamGeo& g, const uint8_
   // the sticky word after it collects every launch's timeouts until cbam_status reads and clears it
   hipError_t e = hipMemsetAsync(ta.counters, 0, g.counters, stream);
   if (e == hipSuccess) e = hipMemsetAsync(ta.err, 0, 4, stream);
-  // the tagged hand-off (RDN_T16_TAGGED) starts from tag 0 in every slot granule: no granule of an
-  // earlier launch can carry a tag this launch waits for
+  // the tagged hand-off (RDN_T16_TAGGED) starts from tag 0 in every slot granule, and each launch
+  // takes tags from a range no earlier launch used (ta.tag0, below): no granule of an earlier launch
+  // -- in memory or left in an XCD's L2 by plain stores (RDN_T16_XCD) -- carries a tag this launch
+  // waits for
   if (e == hipSuccess && mode == MODE_P16 && cb::t16::RDN_T16_TAGGED_ON) e = hipMemsetAsync(ta.slots, 0, g.slots, stream);
   if (e != hipSuccess) return e;
   const int64_t teams = n < g.teams ? n : g.teams;    // never more teams than spectra
   ta.teams = (int)teams;
+  {
+    // CBAMs per team in this launch (ADSDN 17, APIDN 15 per spectrum); tags stay below bit 31
+    // (cbam.hip TAG_OFF_XCD), and the range restarts from 0 when it would reach it
+    static std::atomic<unsigned> next_tag{0};
+    const unsigned span = (unsigned)(((n + teams - 1) / teams) * 17 + 2);
+    unsigned t = next_tag.load(), base;
+    do {
+      base = t + span < 0x7fff0000u ? t : 0u;
+    } while (!next_tag.compare_exchange_weak(t, base + span));
+    ta.tag0 = base;
+  }
   if (mode == MODE_P16) {
     const uint8_t* big16 = blob + pp16_section_offset_arch(arch);
     hipLaunchKernelGGL(team16_kernel(arch), dim3((unsigned)(teams * g.TT)), dim3(THREADS), (uint32_t)team_lds(mode),
