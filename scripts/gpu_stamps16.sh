@@ -2,7 +2,7 @@ set +e
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "(ADSDN or APIDN) and f16 and not f16f8" > gpurun_out/pytest_cbam16.log 2>&1
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "(ADSDN or APIDN) and xcd" > gpurun_out/pytest_cbam16.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|Error|assert" gpurun_out/pytest_cbam16.log | head -10; tail -1 gpurun_out/pytest_cbam16.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 for a in ADSDN APIDN; do
@@ -10,5 +10,5 @@ timeout -k 10 120 python -u tools/team_stamps.py $a f16 10000 stamps > gpurun_ou
 rc=$?; echo "stamps $a rc=$rc"; grep -v amdgpu.ids gpurun_out/stamps16_$a.log | tail -17 | grep -v " 0.000e+00 (  0.0%)"
 if [ $rc -ne 0 ]; then exit $rc; fi
 done
-RDN_ABLATE_ARCH=ADSDN timeout -k 10 300 python -u tools/ablate.py run f16 > gpurun_out/ablate.log 2>&1
+exit 0
 rc=$?; echo "ablate rc=$rc"; grep -v amdgpu.ids gpurun_out/ablate.log | tail -3
