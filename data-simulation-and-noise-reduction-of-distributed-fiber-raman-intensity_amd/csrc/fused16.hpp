@@ -280,17 +280,94 @@ __device__ __forceinline__ void mstep(const Frags& F, int s, V b, Acc& acc) {
 #endif
 }
 
-// Conv1d(1, 64, 3, padding=1) (+ folded BN) + ReLU in fp32: one (row, 16-B slot) item per lane,
-// 640 x 8 items over the workgroup (the slot is wave-uniform, so the weights are scalar loads).
-// ACCUM adds the result onto the resident row (PIDN/train.py:105, identity recomputed from x).
-// out_lo / out_hi (lo <= hi): returns whether any input this thread read at the tile's rows lies
-// outside [lo, hi] (the RDN_F16MIX spiked-tile test, rrcdnet_hybrid.hpp), else false
+// Conv1d(1, 64, 3, padding=1) (+ folded BN) + ReLU in fp32, one (row, 16-B slot) item per lane
+// and step.  ACCUM adds the result onto the resident row (PIDN/train.py:105, identity recomputed
+// from x).  out_lo / out_hi (lo <= hi): returns whether any input this thread read at the tile's
+// rows lies outside [lo, hi] (the RDN_F16MIX spiked-tile test, rrcdnet_hybrid.hpp), else false.
+// RDN_H16_STEM2 (default): wave w computes slot w (8 channels, its 32 weights scalar-loaded once)
+// for rows lane + 64k, and every x value of those rows is fetched before the first is used (buffer
+// loads: positions outside [0, L) read 0 by the range check of the resource) -- one memory latency
+// per stem instead of one per item (the item loop kept the stem on its loads: 7 % of the RDN_F16MIX
+// hybrid, which runs two stems per tile).  Same arithmetic per value as the item loop (bit-equal).
+// RDN_H16_STEM2=2: channel pairs on v_pk_fma_f32 and a packed ReLU after the rounding (no ACCUM)
+#ifndef RDN_H16_STEM2
+#define RDN_H16_STEM2 2
+#endif
 template <bool ACCUM = false>
 __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, float out_lo = 1.f, float out_hi = 0.f) {
   const float* swp = tl.small + sslot * SMALL_SLOT_FLOATS;
   asm volatile("" : "+s"(swp));      // no reuse of scalar-loaded weights across the layers in between
   const cfloat* sw = (const cfloat*)swp;
   bool outside = false;
+#if defined(RDN_ABLATE_NOSTEM)         // diagnostic (tools/ablate.py): the stem's cost, wrong results
+  return outside;
+#endif
+#if RDN_H16_STEM2
+  static_assert(WB % 64 == 0 && WAVES == 8, "one slot per wave, rows lane + 64k");
+  constexpr int NK = WB / 64;
+  const int g = __builtin_amdgcn_readfirstlane(tid() >> 6), lane = tid() & 63;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)tl.x, 0, tl.L * 4, 0x00020000);
+  float xm[NK], x0[NK], xp[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int p = tl.base + lane + 64 * k;
+    xm[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (p - 1), 0, 0));
+    x0[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * p, 0, 0));
+    xp[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (p + 1), 0, 0));
+  }
+  float wb[8], wm[8], w0[8], wp[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = h16_channel(g, j);
+    wb[j] = sw[192 + c];
+    wm[j] = sw[3 * c + 0];
+    w0[j] = sw[3 * c + 1];
+    wp[j] = sw[3 * c + 2];
+  }
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int row = lane + 64 * k;
+    const int p = tl.base + row;
+    const bool valid = in_range(p, tl.L);
+    if (out_lo <= out_hi) outside = outside || x0[k] < out_lo || x0[k] > out_hi;
+    V* ptr = (V*)(tl.lds + dst + soff(row, g));
+    V v;
+#if RDN_H16_STEM2 >= 2
+    if (!ACCUM) {
+      // channel pairs by v_pk_fma_f32 (each half one fmaf, same order), ReLU after the rounding
+      // (rounding is monotone and keeps 0: the same value), rows outside [0, L) zeroed last
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      const f32x2 xm2 = {xm[k], xm[k]}, x02 = {x0[k], x0[k]}, xp2 = {xp[k], xp[k]};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x2 a = {wb[2 * q], wb[2 * q + 1]};
+        a = __builtin_elementwise_fma(f32x2{wm[2 * q], wm[2 * q + 1]}, xm2, a);
+        a = __builtin_elementwise_fma(f32x2{w0[2 * q], w0[2 * q + 1]}, x02, a);
+        a = __builtin_elementwise_fma(f32x2{wp[2 * q], wp[2 * q + 1]}, xp2, a);
+        v[2 * q] = (E)a[0];
+        v[2 * q + 1] = (E)a[1];
+      }
+      v = __builtin_elementwise_max(v, (V)((E)0.f));
+      if (!valid) v = (V)((E)0.f);
+      *ptr = v;
+      continue;
+    }
+#endif
+    if (ACCUM) v = *ptr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float a = wb[j];
+      a = fmaf(wm[j], xm[k], a);
+      a = fmaf(w0[j], x0[k], a);
+      a = fmaf(wp[j], xp[k], a);
+      a = fmaxf(a, 0.f);
+      if (ACCUM) a += (float)v[j];
+      v[j] = (E)(valid ? a : 0.f);
+    }
+    *ptr = v;
+  }
+  return outside;
+#endif
   for (int i = tid(); i < WB * 8; i += THREADS) {
     const int g = __builtin_amdgcn_readfirstlane(i / WB);
     const int row = i - g * WB;
