@@ -239,3 +239,31 @@ def test_exact_accumulator_allreduce_world2_gloo():
         two = out["sums"]
     assert one == two
     np.testing.assert_allclose(np.array(one[:4]) / one[4], per.mean(axis=0), rtol=1e-13)
+
+
+def _team16_place(wg, teams, TT):
+    """cbam.hip team16_forward's workgroup -> (team, tile, one-XCD candidate), restated: workgroups
+    8r + x (r < R0 = tpx TT) form teams 8j + x (r = j TT + tile), the rest the remaining teams in order"""
+    tpx = (teams * TT // 8) // TT
+    R0 = tpx * TT
+    if wg < 8 * R0:
+        x, r = wg & 7, wg >> 3
+        return (r // TT) * 8 + x, r % TT, x
+    i = wg - 8 * R0
+    return 8 * tpx + i // TT, i % TT, None
+
+
+@pytest.mark.parametrize("teams,TT", [(16, 16), (9, 27), (1, 16), (3, 16), (8, 32), (12, 21), (2, 27), (5, 51)])
+def test_team16_xcd_placement_is_a_bijection(teams, TT):
+    """Every (team, tile) of the launch is owned by exactly one workgroup, and every team formed from
+    workgroups 8r + x lies on one round-robin XCD x (L = 10,000: 16 one-XCD teams of 16; L = 16,384:
+    8 of 27 plus one spread team)."""
+    seen, xcd = {}, {}
+    for wg in range(teams * TT):
+        team, tile, x = _team16_place(wg, teams, TT)
+        assert 0 <= team < teams and 0 <= tile < TT
+        assert (team, tile) not in seen
+        seen[(team, tile)] = wg
+        if x is not None:
+            assert wg % 8 == x and xcd.setdefault(team, x) == x
+    assert len(seen) == teams * TT
