@@ -461,6 +461,10 @@ __device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[Hea
   using TG = TileGeo<NBK>;
   const cfloat* hw = small_slot(tl, slot);
   if constexpr (HeadOut<MODE, NBK>::VEC) {
+#if defined(RDN_ABLATE_NOHEADV)       // diagnostic (tools/ablate.py): the vectorized head's cost, wrong output
+    for (int k = 0; k < NBK; ++k) out[k] = 0.0;
+    return;
+#endif
     const int tid = opaque_tid(), lane = tid & 63, w = tid >> 6, q = lane >> 4, c16 = lane & 15;
     // channel of element jj of 16-B f16 slot s: h16_channel order (f16 + e4m3 tile), natural otherwise
     auto chan = [&](int s, int jj) { return MODE == MODE_H8 ? h16_channel(s, jj) : 8 * s + jj; };
