@@ -2,19 +2,23 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--arch RRCDNet] [--dtype f16] [--batch B]
 
-The headline dtype is f16: one v_mfma_f32_16x16x32_f16 per product (the bf16 MFMA rate) on f16
-weights and activations with fp32 accumulation -- the engine's fastest mode within the north-star
-16-bit tolerance (2e-2 max-abs; worst measured 1.6e-2, trained RRCDNet, tests/test_forward_gpu.py).
+The headline dtype is 'f16', the engine's fastest mode within the north-star 16-bit tolerance
+(2e-2 max-abs): on RRCDNet that is RDN_F16MIX -- one v_mfma_f32_16x16x32_f16 per product (the bf16
+MFMA rate) on f16 weights and activations with fp32 accumulation on 24 of the 29 64-channel layers,
+the last five right-branch layers with the block-scaled e4m3 correction (parity in
+profiles/r04/parity_table.md).
 The f16 + e4m3-correction mode (f16f8, ~15 significant bits), split bf16 (bf16x3), single-rounding
 bf16 ('bf16-unsafe', NOT within 2e-2 on trained RRCDNet) and fp32 (compensated, within 1e-5) are
 timed as "variants" in the same line.
 
 One step = one forward of the fused network over a batch of B synthetic spectra per GPU (L = 10000),
 generated on-device by the engine's simulator BEFORE the timed region (inputs resident in HBM).
-Data-parallel over N GPUs, one process per GPU (torch.distributed.run): every rank simulates its
-own spectrum-index range, so per-GPU work is fixed as N grows ("weak" scaling); the only
-collective is the end-of-run metric all-reduce (outside the timed region), plus the timing
-barrier/max.  Rank 0 prints ONE JSON line.
+Data-parallel over N GPUs, one process per GPU (torch.distributed.run; `python bench.py --gpus N`
+without a launcher starts it itself, before any GPU call): every rank simulates its own
+spectrum-index range (index_blocks: headline, pipeline and config-4 blocks disjoint across ranks and
+legs), so per-GPU work is fixed as N grows ("weak" scaling); the only collective is the end-of-run
+metric all-reduce (outside the timed region), plus the timing barrier/max.  Rank 0 prints ONE JSON
+line.
 """
 import argparse
 import json
@@ -38,7 +42,7 @@ LAYERS = {"DenoiseCNN": (18, 1, 1), "RRCDNet": (29, 2, 2), "DSDN": (32, 1, 1), "
           "ADSDN": (32, 1, 1), "APIDN": (30, 1, 1)}
 SA_CONVS = {"ADSDN": 17, "APIDN": 15}
 # MFMA cycles per product relative to one bf16 MFMA (v_mfma_f32_16x16x32_bf16 = 16 cycles per K=32)
-# ('f16' on RRCDNet = RDN_F16MIX: 26 plain layers + 3 corrected at 2 units, bench.mfma_cost)
+# ('f16' on RRCDNet = RDN_F16MIX: 24 plain layers + 5 corrected at 2 units, bench.mfma_cost)
 MFMA_COST = {"f16": 1, "f16-plain": 1, "bf16-unsafe": 1, "bf16x3": 3, "f16f8": 2}
 
 
@@ -62,6 +66,34 @@ def flops_per_spectrum(arch, L):
     big, stems, heads = LAYERS[arch]
     per_pos = big * 2 * 64 * 64 * 3 + stems * 2 * 64 * 3 + heads * 2 * 64 * 3 + SA_CONVS.get(arch, 0) * 2 * 2 * 7
     return per_pos * L
+
+
+def index_blocks(world, rank, B, steps_pipeline=3, B4=8192, chunks4=4):
+    """Simulator spectrum indices each leg of rank `rank` generates (half-open ranges): the headline
+    batch, the pipeline's steps + 1 batches, and the config-4 driver's total (evaluate_synthetic
+    shards [first, first + total) over the ranks itself).  Disjoint across legs and ranks."""
+    head = (rank * B, (rank + 1) * B)
+    p0 = world * B + rank * (steps_pipeline + 1) * B
+    pipe = (p0, p0 + (steps_pipeline + 1) * B)
+    c4first = world * B + world * (steps_pipeline + 1) * B
+    c4total = world * chunks4 * B4
+    return {"headline": head, "pipeline": pipe, "config4_first": c4first, "config4_total": c4total,
+            "config4_warmup_first": c4first + c4total}
+
+
+def launch_ranks(n, argv):
+    """`python bench.py --gpus N` without a launcher: start N ranks under torch.distributed.run
+    (127.0.0.1 rendezvous) as a child process and return its exit code.  Called before anything
+    touches the GPU (torch.cuda.device_count() does not initialise it on this image)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + argv
+    progress(f"launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd)
 
 
 def progress(msg):
@@ -281,7 +313,7 @@ def _model(R, arch, dtype, dev, trained=True):
     return m.to(dev).eval().set_engine_dtype(dtype), src
 
 
-def config_keys(R, engine, args, dev, stream, world, rank):
+def config_keys(R, engine, args, dev, stream, world, rank, blocks):
     """BASELINE.json configs 2, 4 and 5 as extra keys of the bench line (each labelled with its own
     configs[i]), on the trained golden fixture weights.  Config 4 runs at every world size (the
     data-parallel driver: rank r owns [r*N/W, (r+1)*N/W), exact metric sums all-reduced, so its means
@@ -293,11 +325,14 @@ def config_keys(R, engine, args, dev, stream, world, rank):
     B4 = args.config4_batch
     total = world * args.config4_chunks * B4
     models = {a: _model(R, a, args.dtype, dev)[0] for a in args.config4_archs.split(",")}
+    assert total == blocks["config4_total"]
     evaluate_synthetic({a: m for a, m in models.items()}, world * 2, seed=args.seed, signal_length=L,
-                       batch_size=2, device=dev)                                   # warm-up (pack, first launch)
+                       batch_size=2, device=dev, first_index=blocks["config4_warmup_first"])  # warm-up (pack, launch)
     progress(f"config 4: {total} spectra x {len(models)} networks")
-    res = evaluate_synthetic(models, total, seed=args.seed, signal_length=L, batch_size=B4, device=dev)
+    res = evaluate_synthetic(models, total, seed=args.seed, signal_length=L, batch_size=B4, device=dev,
+                             first_index=blocks["config4_first"])
     cfg4 = {"config": "BASELINE.json configs[3]", "total_spectra": total, "batch_per_gpu": B4,
+            "first_index": blocks["config4_first"],
             "dtype": args.dtype, "signal_length": L, "n_gpus": world,
             "note": "evaluate_synthetic: per chunk on-device simulate -> fused forward -> exact metric sums; rank r "
                     "owns spectrum indices [r*N/W, (r+1)*N/W); the accumulators are all-reduced once (means "
@@ -380,6 +415,11 @@ def main():
                     help="nccl (RCCL over xGMI, one rank per GPU); gloo rehearses the N>1 path with ranks "
                          "sharing the visible GPUs (collectives staged through host memory)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if args.dist_backend == "nccl" and args.gpus > torch.cuda.device_count():
+            raise SystemExit(f"--gpus {args.gpus}: only {torch.cuda.device_count()} GPU(s) visible; one RCCL rank "
+                             "per GPU (rehearse more ranks with --dist-backend gloo)")
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -413,7 +453,8 @@ def main():
     torch.manual_seed(1234)                       # random-init weights of the architecture
     model = R.MODELS[args.arch]().to(dev).eval().set_engine_dtype(args.dtype)
     B, L = args.batch, args.L
-    clean, noisy, _, _ = engine.generate(B, args.seed, first_index=rank * B, signal_length=L, device=dev)
+    blocks = index_blocks(world, rank, B, 3, args.config4_batch, args.config4_chunks)
+    clean, noisy, _, _ = engine.generate(B, args.seed, first_index=blocks["headline"][0], signal_length=L, device=dev)
     x = noisy.view(B, 1, L)
     y = torch.empty_like(x)
     packed = model.packed_weights(dev)
@@ -487,14 +528,13 @@ def main():
     pipeline = None
     if not args.no_pipeline:
         progress("pipeline")
-        # indices [0, world*B) fed the headline; each rank's pipeline block of 4*B indices follows,
-        # disjoint across ranks (rank r once re-generated rank r+1's steps)
-        pipeline = time_pipeline(engine, args.arch, code, packed, args.seed, world * B + rank * 4 * B, B, L,
+        # each rank's pipeline block of 4*B indices after every rank's headline batch (index_blocks)
+        pipeline = time_pipeline(engine, args.arch, code, packed, args.seed, blocks["pipeline"][0], B, L,
                                  3, stream, dev)
 
     configs = None
     if not args.no_configs:
-        configs = config_keys(R, engine, args, dev, stream, world, rank)
+        configs = config_keys(R, engine, args, dev, stream, world, rank, blocks)
 
     if rank == 0:
         total = world * B * args.steps

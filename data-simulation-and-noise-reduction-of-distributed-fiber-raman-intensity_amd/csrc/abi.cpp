@@ -23,14 +23,16 @@ hipError_t launch_fused16(int arch, const uint8_t* blob, const float* x, float* 
 hipError_t launch_fused16_f16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
 hipError_t launch_fused16_f16_small(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                    hipStream_t s);
-hipError_t launch_fused_inplace_short(const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
+hipError_t launch_fused_inplace_short(const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
+                                      hipStream_t s);
 hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
-                                hipStream_t s);
+                                unsigned* status, hipStream_t s);
 
 hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                void* ws, size_t ws_bytes, hipStream_t s);
 size_t cbam_workspace_bytes(int arch, int dtype, int64_t n, int64_t L, hipStream_t s);
-hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t s, int* timed_out);
+hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t s, int* timed_out,
+                       int* out_of_range);
 hipError_t cbam_workspace_init(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t s);
 hipError_t launch_generate(uint64_t seed, uint64_t first, int64_t n, int L, float snr_lo, float snr_hi, float extreme_prob,
                            int max_repeat, float* clean, float* noisy, float* snr, float* nstd, hipStream_t s);
@@ -55,6 +57,14 @@ int hip_check(hipError_t e, const char* what) {
 bool valid_arch(int a) { return a >= RDN_DENOISECNN && a <= RDN_APIDN; }
 bool valid_dtype(int d) { return d >= RDN_F32 && d <= RDN_F16MIX; }
 bool is_cbam(int a) { return a == RDN_ADSDN || a == RDN_APIDN; }
+// the dtypes whose e4m3 correction planes bound the activations (RDN_ERANGE, inplace.hpp range_vote);
+// the fused networks keep their range word in the first 4 bytes of a RANGE_WS_BYTES workspace
+bool range_checked(int d) { return d == RDN_F16F8 || d == RDN_F16MIX; }
+constexpr size_t RANGE_WS_BYTES = 256;
+const char* range_msg() {
+  return "an activation left the range of the e4m3 correction planes (|v| > 1792, RDN_F16F8 / RDN_F16MIX): the "
+         "affected tiles' outputs are NaN; inputs this large need RDN_F32 or RDN_BF16X3";
+}
 // RDN_F16MIX exists for RRCDNet only (checked before any per-network dispatch)
 bool unsupported(int arch, int dtype) { return dtype == RDN_F16MIX && arch != RDN_RRCDNET; }
 int fail_unsupported(const char* fn) {
@@ -172,7 +182,8 @@ int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes,
   if (!valid_arch(arch) || !valid_dtype(dtype) || !bytes || n < 0 || L < 1)
     return fail(RDN_EINVAL, "rdn_workspace_size: bad argument");
   if (unsupported(arch, dtype)) return fail_unsupported("rdn_workspace_size");
-  *bytes = is_cbam(arch) ? rdn::cbam_workspace_bytes(arch, dtype, n, L, (hipStream_t)stream) : 0;
+  *bytes = is_cbam(arch) ? rdn::cbam_workspace_bytes(arch, dtype, n, L, (hipStream_t)stream)
+                          : range_checked(dtype) ? RANGE_WS_BYTES : 0;
   return RDN_OK;
   RDN_GUARD_END
 }
@@ -182,8 +193,13 @@ int rdn_workspace_init(int arch, int dtype, int64_t n, int64_t L, void* ws, size
   if (!valid_arch(arch) || !valid_dtype(dtype) || n < 0 || L < 1 || L > 0x7fffffff)
     return fail(RDN_EINVAL, "rdn_workspace_init: bad argument");
   if (unsupported(arch, dtype)) return fail_unsupported("rdn_workspace_init");
-  if (!is_cbam(arch)) return RDN_OK;
   const hipStream_t s = (hipStream_t)stream;
+  if (!is_cbam(arch)) {
+    if (!range_checked(dtype)) return RDN_OK;
+    if (!ws || ws_bytes < RANGE_WS_BYTES)
+      return fail(RDN_ESIZE, "rdn_workspace_init: workspace too small, need " + std::to_string(RANGE_WS_BYTES) + " bytes");
+    return hip_check(hipMemsetAsync(ws, 0, 4, s), "rdn_workspace_init");
+  }
   const size_t need = rdn::cbam_workspace_bytes(arch, dtype, n, L, s);
   if (ws_bytes < need || (need && !ws))
     return fail(RDN_ESIZE, "rdn_workspace_init: workspace too small, need " + std::to_string(need) + " bytes");
@@ -224,13 +240,15 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
     return hip_check(rdn::launch_cbam_forward(arch, dtype, blob, x, y, n, (int)L, ws, ws_bytes, s), "cbam forward");
   }
   if (dtype == RDN_BF16) return hip_check(rdn::launch_fused16(arch, blob, x, y, n, (int)L, s), "fused bf16 forward");
+  // range word of RDN_F16F8 / RDN_F16MIX (optional: without a workspace a saturated tile still writes NaN)
+  unsigned* status = range_checked(dtype) && ws && ws_bytes >= RANGE_WS_BYTES ? (unsigned*)ws : nullptr;
   const bool shrt = short_tiles(arch, n, L, s);
   if (dtype == RDN_F16)
     return hip_check(shrt ? rdn::launch_fused16_f16_small(arch, blob, x, y, n, (int)L, s)
                           : rdn::launch_fused16_f16(arch, blob, x, y, n, (int)L, s), "fused f16 forward");
   if (dtype == RDN_F16MIX && shrt)
-    return hip_check(rdn::launch_fused_inplace_short(blob, x, y, n, (int)L, s), "fused f16mix forward (short tiles)");
-  return hip_check(rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, s), "fused in-place forward");
+    return hip_check(rdn::launch_fused_inplace_short(blob, x, y, n, (int)L, status, s), "fused f16mix forward (short tiles)");
+  return hip_check(rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, status, s), "fused in-place forward");
   RDN_GUARD_END
 }
 
@@ -240,18 +258,30 @@ int rdn_forward_status(int arch, int dtype, int64_t n, int64_t L, void* ws, size
   if (n < 0 || L < 1 || L > 0x7fffffff) return fail(RDN_EINVAL, "rdn_forward_status: bad n / L");
   if (unsupported(arch, dtype)) return fail_unsupported("rdn_forward_status");
   const hipStream_t s = (hipStream_t)stream;
-  if (!is_cbam(arch) || n == 0) return hip_check(hipStreamSynchronize(s), "rdn_forward_status");
+  if (!is_cbam(arch)) {
+    int rc = hip_check(hipStreamSynchronize(s), "rdn_forward_status");
+    if (rc != RDN_OK || !range_checked(dtype) || !ws || ws_bytes < RANGE_WS_BYTES) return rc;
+    unsigned w = 0;
+    rc = hip_check(hipMemcpy(&w, ws, sizeof(w), hipMemcpyDeviceToHost), "rdn_forward_status");
+    if (rc != RDN_OK) return rc;
+    if (!w) return RDN_OK;
+    rc = hip_check(hipMemset(ws, 0, 4), "rdn_forward_status");
+    return rc != RDN_OK ? rc : fail(RDN_ERANGE, range_msg());
+  }
+  if (n == 0) return hip_check(hipStreamSynchronize(s), "rdn_forward_status");
   const size_t need = rdn::cbam_workspace_bytes(arch, dtype, n, L, s);
   if (ws_bytes < need || (need && !ws))
     return fail(RDN_ESIZE, "rdn_forward_status: workspace smaller than this device's CBAM geometry needs (" +
                                std::to_string(need) + " bytes)");
-  int timed_out = 0;
-  const int rc = hip_check(rdn::cbam_status(arch, dtype, L, ws, ws_bytes, s, &timed_out), "rdn_forward_status");
+  int timed_out = 0, out_of_range = 0;
+  const int rc = hip_check(rdn::cbam_status(arch, dtype, L, ws, ws_bytes, s, &timed_out, &out_of_range),
+                           "rdn_forward_status");
   if (rc != RDN_OK) return rc;
   if (timed_out)
     return fail(RDN_EHIP, "CBAM team hand-off timed out: a workgroup of a spectrum's team never arrived (the "
                           "grid's co-residency was broken, e.g. by a concurrent kernel on the device); the "
                           "affected spectra's outputs are NaN");
+  if (out_of_range) return fail(RDN_ERANGE, range_msg());
   return RDN_OK;
   RDN_GUARD_END
 }

@@ -54,6 +54,7 @@ struct Seg {
   float* u_out;
   double* sum_out;
   unsigned* max_out;
+  unsigned* range;              // MODE_H8 range guard words: [0] this forward, [1] sticky (cbam_status)
 };
 
 __device__ __forceinline__ unsigned f2ord(float f) {
@@ -174,7 +175,7 @@ __device__ void prologue_cbam(Tile& tl, const Seg& sg, int n) {
       }
       if (sg.store_h && r >= H && r < H + T) *(f32x4*)(sg.h_out + off) = h;
     }
-    Op<MODE>::store4(lds, r + GUARD, 4 * sub, h);
+    Op<MODE>::store4(lds, r + GUARD, 4 * sub, h, &tl.amax);
   }
 }
 
@@ -262,6 +263,13 @@ __global__ __launch_bounds__(THREADS) void segment(const uint8_t* __restrict__ b
     if ((i ? sg.epi1 : sg.epi0) & RELU) conv<MODE, RELU, G::S>(tl, 1, id, a, more);
     else conv<MODE, 0, G::S>(tl, 1, id, a, more);
   }
+  // MODE_H8 range guard (inplace.hpp range_vote): a saturated tile raises this forward's word and the
+  // sticky one; the head segment writes NaN if any segment of the forward saturated
+  bool sat = false;
+  if constexpr (MODE == MODE_H8) {
+    sat = range_vote(tl, RED_OFF, sg.range + 1);
+    if (sat && __builtin_amdgcn_workitem_id_x() == 0) __hip_atomic_store(sg.range, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (sg.epi == EPI_STORE) {
     epilogue_store<MODE>(tl, sg, n);
     return;
@@ -277,6 +285,9 @@ __global__ __launch_bounds__(THREADS) void segment(const uint8_t* __restrict__ b
   if (sg.head_sigmoid) {
 #pragma unroll
     for (int k = 0; k < HeadOut<MODE>::ROWS; ++k) v[k] = sigm(v[k]);
+  }
+  if constexpr (MODE == MODE_H8) {
+    if (sat || __hip_atomic_load(sg.range, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) nan_rows(v);
   }
   store_out<MODE>(tl, y, n, v, sg.halo, T);
 }
@@ -575,7 +586,7 @@ template <int MODE> constexpr int ID_PRE = MODE == MODE_X3 ? 8 : 16;
 #endif
 
 template <int MODE>
-__device__ __forceinline__ void apply_cbam(const Tile& tl, const TeamArgs& ta, const char* slots0, int cbam_slot, bool bias, int res,
+__device__ __forceinline__ void apply_cbam(Tile& tl, const TeamArgs& ta, const char* slots0, int cbam_slot, bool bias, int res,
                            bool save_next, __amdgpu_buffer_rsrc_t hs, Stamps& st) {
   char* lds = tl.lds;
   float* s1 = (float*)(lds + S1_OFF) + 3;       // index -3 .. 514
@@ -741,7 +752,7 @@ __device__ __forceinline__ void apply_cbam(const Tile& tl, const TeamArgs& ta, c
     }
     const int p = tl.base + r;
     if (p < 0 || p >= tl.L) h = f32x4{0.f, 0.f, 0.f, 0.f};
-    Op<MODE>::store4(lds, r + GUARD, 4 * sub, h);
+    Op<MODE>::store4(lds, r + GUARD, 4 * sub, h, &tl.amax);
     if (save_next) id_store<MODE>(lds, hs, r, sub, h);
   }
   __syncthreads();
@@ -776,6 +787,7 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
     tl.big = blob + SMALL_BYTES;
     tl.layer = 0;
     tl.corr = corr_mask(blob);
+    tl.amax = 0.f;
     LayerA<MODE> a;
     load_layer_a<MODE>(tl, 0, a);
     // stats of u -> team -> apply.  The identity rows are fetched while the team assembles; the
@@ -834,6 +846,11 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
     if (__hip_atomic_load(ta.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
 #pragma unroll
       for (int k = 0; k < HeadOut<MODE>::ROWS; ++k) v[k] = __uint_as_float(0x7fc00000u);   // quiet NaN (bit pattern: -fno-honor-nans build)
+    }
+    // MODE_H8 range guard: a tile whose activations saturated raises the sticky range word (err[2],
+    // the authoritative signal: its CBAM statistics reached the whole team) and writes NaN
+    if constexpr (MODE == MODE_H8) {
+      if (range_vote(tl, RED_OFF, ta.err + 2)) nan_rows(v);
     }
     store_out<MODE>(tl, y, (int)n, v, ta.halo, ta.T);
     __syncthreads();                 // the next spectrum's stem overwrites the rows the head read
@@ -1659,6 +1676,10 @@ __global__ __launch_bounds__(h16c::THREADS) void team16_forward(const uint8_t* _
 static constexpr int64_t CBAM_CHUNK = 1024;       // spectra per pass (bounds the workspace)
 
 static size_t act_bytes(int64_t n, int64_t L) { return (size_t)n * L * 64 * sizeof(float); }
+// The segment path's workspace: [256 B status: the MODE_H8 range words, [0] this forward's chunk, [1]
+// sticky (cbam_status)] [4 activation buffers] [2 x statistics], 256-B aligned
+static char* seg_base(void* ws) { return (char*)(((uintptr_t)ws + 255) & ~(uintptr_t)255); }
+static unsigned* seg_range(void* ws) { return (unsigned*)seg_base(ws); }
 
 // Team-persistent geometry: TEAM_HALO rows per side (refreshed from the neighbours at every CBAM),
 // TT tiles per spectrum, as many teams as the device holds co-resident: the occupancy API's
@@ -1741,7 +1762,7 @@ size_t cbam_workspace_bytes(int arch, int dtype, int64_t n, int64_t L, hipStream
   const TeamGeo g = team_geo(arch, team_mode(dtype), L, stream_device(stream));
   if (g.teams > 0) return g.total;
   const int64_t c = n < CBAM_CHUNK ? n : CBAM_CHUNK;
-  return 4 * act_bytes(c, L) + 2 * (size_t)c * 64 * (sizeof(double) + sizeof(unsigned)) + 256;
+  return 256 + 4 * act_bytes(c, L) + 2 * (size_t)c * 64 * (sizeof(double) + sizeof(unsigned)) + 256;
 }
 
 // workspace carve-up of the team kernel: slots | counters | identity buffers | error word | stamps
@@ -1829,7 +1850,7 @@ hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const f
   const bool adsdn = arch == ADSDN;
   const int64_t chunk = n < CBAM_CHUNK ? n : CBAM_CHUNK;
   if (ws_bytes < cbam_workspace_bytes(arch, dtype, chunk, L, stream)) return hipErrorInvalidValue;
-  char* base = (char*)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
+  char* base = seg_base(ws) + 256;
   float* act[4];
   for (int i = 0; i < 4; ++i) act[i] = (float*)(base + i * act_bytes(chunk, L));
   double* sums[2];
@@ -1840,10 +1861,16 @@ hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const f
     maxs[i] = (unsigned*)(st + 2 * chunk * 64 * 8 + i * chunk * 64 * 4);
   }
 
+  unsigned* range = seg_range(ws);
   for (int64_t n0 = 0; n0 < n; n0 += chunk) {
     const int64_t nn = n - n0 < chunk ? n - n0 : chunk;
     const float* xs = x + n0 * L;
     float* ys = y + n0 * L;
+    // this chunk's range word starts clear (the sticky word behind it is cleared by cbam_status)
+    if (mode == ip::MODE_H8) {
+      const hipError_t er = hipMemsetAsync(range, 0, 4, stream);
+      if (er != hipSuccess) return er;
+    }
     // segment list (ADSDN/train.py:160-167, APIDN/train.py:150-159)
     std::vector<Seg> segs;
     auto mk = [&](int pro, int res, int store_h, int slot, int nconv, int e0, int e1, int layer0, int epi) {
@@ -1851,6 +1878,7 @@ hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const f
       s.pro = pro; s.res = res; s.store_h = store_h; s.cbam_slot = slot; s.bias = adsdn;
       s.n_convs = nconv; s.epi0 = e0; s.epi1 = e1; s.layer0 = layer0; s.epi = epi;
       s.head_slot = 1; s.head_sigmoid = !adsdn; s.head_add_stem = !adsdn;
+      s.range = range;
       s.halo = nconv + (epi == EPI_HEAD ? 1 : 0);
       return s;
     };
@@ -1893,29 +1921,48 @@ hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const f
   return hipSuccess;
 }
 
-// A new workspace: clear the team kernel's sticky hand-off error word (the caller checked the size).
+// A new workspace: clear the sticky status words -- the team kernel's hand-off error word and range
+// word (err[1], err[2]), or the segment path's range word (the caller checked the size).
 hipError_t cbam_workspace_init(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t stream) {
   const TeamGeo tg = team_geo(arch, team_mode(dtype), L, stream_device(stream));
-  if (tg.teams <= 0) return hipSuccess;                                 // segment path: no hand-off
+  if (tg.teams <= 0) {
+    if (!ws) return hipSuccess;
+    return hipMemsetAsync(seg_range(ws), 0, 8, stream);
+  }
   if (!ws || ws_bytes < tg.total) return hipErrorInvalidValue;
-  return hipMemsetAsync(team_err(tg, ws) + 1, 0, 4, stream);          // the sticky word
+  return hipMemsetAsync(team_err(tg, ws) + 1, 0, 8, stream);          // the sticky words
 }
 
-// After CBAM forwards on `stream`: wait for them, then read and clear the team kernel's sticky
-// hand-off error word.  *timed_out = 1 if a team wait of any forward since the last read exceeded
-// its spin limit (outputs of affected spectra are NaN).  The caller checked the workspace size.
-hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t stream, int* timed_out) {
+// After CBAM forwards on `stream`: wait for them, then read and clear the sticky status words.
+// *timed_out = 1 if a team wait of any forward since the last read exceeded its spin limit (outputs
+// of affected spectra are NaN); *out_of_range = 1 if a MODE_H8 activation saturated.  The caller
+// checked the workspace size.
+hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t stream,
+                       int* timed_out, int* out_of_range) {
   *timed_out = 0;
+  *out_of_range = 0;
   hipError_t e = hipStreamSynchronize(stream);
   if (e != hipSuccess) return e;
   const TeamGeo tg = team_geo(arch, team_mode(dtype), L, stream_device(stream));
-  if (tg.teams <= 0) return hipSuccess;                                 // segment path: no hand-off
-  if (!ws || ws_bytes < tg.total) return hipErrorInvalidValue;
-  unsigned err = 0;
-  e = hipMemcpy(&err, team_err(tg, ws) + 1, sizeof(err), hipMemcpyDeviceToHost);     // the sticky word
+  unsigned* words;
+  if (tg.teams <= 0) {
+    if (!ws) return hipSuccess;
+    words = seg_range(ws);                                              // [0] forward, [1] sticky
+  } else {
+    if (!ws || ws_bytes < tg.total) return hipErrorInvalidValue;
+    words = team_err(tg, ws);                                           // [1] timeout, [2] range (sticky)
+  }
+  unsigned w[3] = {0, 0, 0};
+  e = hipMemcpy(w, words, sizeof(w), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return e;
-  *timed_out = err != 0;
-  if (err) e = hipMemset(team_err(tg, ws) + 1, 0, 4);
+  if (tg.teams <= 0) {
+    *out_of_range = w[1] != 0;
+    if (w[1]) e = hipMemset(words + 1, 0, 4);
+  } else {
+    *timed_out = w[1] != 0;
+    *out_of_range = w[2] != 0;
+    if (w[1] || w[2]) e = hipMemset(words + 1, 0, 8);
+  }
   return e;
 }
 

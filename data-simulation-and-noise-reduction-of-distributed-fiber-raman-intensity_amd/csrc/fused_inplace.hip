@@ -26,7 +26,16 @@ namespace ip {
 // spectrum), whose rows every write-back re-zeroes; interior tiles skip that per-row select.
 #define IP_BODY(name) \
   template <int MODE, bool EDGE, int NBK, int TAIL> \
-  __device__ __forceinline__ void name##_body(Tile& tl, float* y, int n, int L, int T)
+  __device__ __forceinline__ void name##_body(Tile& tl, float* y, int n, int L, int T, unsigned* status)
+
+// MODE_H8 (RDN_F16F8 / RDN_F16MIX) bodies end with the range vote (inplace.hpp range_vote): a tile
+// whose activations left the e4m3 planes' range writes NaN and raises the status word
+template <int MODE, int N>
+__device__ __forceinline__ void range_guard(const Tile& tl, unsigned* status, float (&o)[N]) {
+  if constexpr (MODE == MODE_H8) {
+    if (range_vote(tl, 0, status)) nan_rows(o);
+  }
+}
 
 // RRCDNet's right-branch head outputs are parked in y (as fp32) over the left branch in the
 // vectorized-head modes, whose 5 double rows per lane would otherwise hold 10 VGPRs through it
@@ -68,6 +77,7 @@ IP_BODY(denoisecnn) {
   head<MODE, NBK>(tl, 1, d);
   float o[HeadOut<MODE, NBK>::ROWS];
   round_rows(d, o);
+  range_guard<MODE>(tl, status, o);
   store_out<MODE, NBK>(tl, y, n, o, H, T);
 }
 
@@ -117,6 +127,7 @@ IP_BODY(rrcdnet) {
     const double rv = HO::VEC ? parked_row<MODE, NBK>(tl, y, n, k, H, T) : r[k];
     o[k] = (float)((double)xv - (rv + l[k]) * 0.5);
   }
+  range_guard<MODE>(tl, status, o);
   store_out<MODE, NBK>(tl, y, n, o, H, T);
 }
 
@@ -139,6 +150,7 @@ IP_BODY(dsdn) {
   head<MODE, NBK>(tl, 1, d);
   float o[HeadOut<MODE, NBK>::ROWS];
   round_rows(d, o);
+  range_guard<MODE>(tl, status, o);
   store_out<MODE, NBK>(tl, y, n, o, H, T);
 }
 
@@ -163,6 +175,7 @@ IP_BODY(pidn) {
   round_rows(d, o);
 #pragma unroll
   for (int k = 0; k < HeadOut<MODE, NBK>::ROWS; ++k) o[k] = 1.0f / (1.0f + expf(-o[k]));
+  range_guard<MODE>(tl, status, o);
   store_out<MODE, NBK>(tl, y, n, o, H, T);
 }
 
@@ -221,8 +234,8 @@ __device__ __forceinline__ void nan_outputs(const Tile& tl, float* y, int n, int
 // The all-corrected body of a spiked tile (RDN_F16F8 on the RDN_F16MIX blob, which carries every
 // layer's e4m3 correction fragments)
 template <bool EDGE, int NBK>
-__device__ __forceinline__ void rrcdnet_f16f8_tile(Tile& tl, float* y, int n, int L, int T) {
-  rrcdnet_body<MODE_H8, EDGE, NBK, 0>(tl, y, n, L, T);
+__device__ __forceinline__ void rrcdnet_f16f8_tile(Tile& tl, float* y, int n, int L, int T, unsigned* status) {
+  rrcdnet_body<MODE_H8, EDGE, NBK, 0>(tl, y, n, L, T, status);
 }
 
 // Whether any input of the tile's rows [base, base + WB) inside [0, L) lies outside [lo, hi]
@@ -254,23 +267,24 @@ __device__ __forceinline__ bool window_outside(const Tile& tl, float lo, float h
 // whose input window leaves [F16MIX_WIN_LO, F16MIX_WIN_HI] (a spike) runs every layer corrected
 template <int TAIL>
 __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restrict__ blob, const float* __restrict__ x,
-                                                          float* __restrict__ y, int L, int T, int tiles) {
+                                                          float* __restrict__ y, int L, int T, int tiles,
+                                                          unsigned* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
   if (!f16mix_blob_ok(blob)) return nan_outputs(tl, y, n, T);
   const int need = L - tl.base + 2;
   if (tl.base >= 0 && tl.base + TileGeo<5>::WB <= L) {
-    if (!hyb640::rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles))
-      rrcdnet_f16f8_tile<false, 5>(tl, y, n, L, T);                // spiked tile: every layer corrected
+    if (!hyb640::rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles, status))
+      rrcdnet_f16f8_tile<false, 5>(tl, y, n, L, T, status);        // spiked tile: every layer corrected
   } else if (need <= 512) {
     // short last tile (the in-place body on the fewest blocks): all layers corrected when spiked
     const bool spiked = window_outside(tl, F16MIX_WIN_LO, F16MIX_WIN_HI);
-    if (need <= 256) spiked ? rrcdnet_f16f8_tile<true, 2>(tl, y, n, L, T) : rrcdnet_body<MODE_H8, true, 2, TAIL>(tl, y, n, L, T);
-    else if (need <= 384) spiked ? rrcdnet_f16f8_tile<true, 3>(tl, y, n, L, T) : rrcdnet_body<MODE_H8, true, 3, TAIL>(tl, y, n, L, T);
-    else spiked ? rrcdnet_f16f8_tile<true, 4>(tl, y, n, L, T) : rrcdnet_body<MODE_H8, true, 4, TAIL>(tl, y, n, L, T);
-  } else if (!hyb640::rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles)) {
-    rrcdnet_f16f8_tile<true, 5>(tl, y, n, L, T);
+    if (need <= 256) spiked ? rrcdnet_f16f8_tile<true, 2>(tl, y, n, L, T, status) : rrcdnet_body<MODE_H8, true, 2, TAIL>(tl, y, n, L, T, status);
+    else if (need <= 384) spiked ? rrcdnet_f16f8_tile<true, 3>(tl, y, n, L, T, status) : rrcdnet_body<MODE_H8, true, 3, TAIL>(tl, y, n, L, T, status);
+    else spiked ? rrcdnet_f16f8_tile<true, 4>(tl, y, n, L, T, status) : rrcdnet_body<MODE_H8, true, 4, TAIL>(tl, y, n, L, T, status);
+  } else if (!hyb640::rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles, status)) {
+    rrcdnet_f16f8_tile<true, 5>(tl, y, n, L, T, status);
   }
 }
 
@@ -278,33 +292,36 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restr
 // latency geometry for launches too small to fill the chip (launch_fused_inplace_short)
 template <int TAIL>
 __global__ __launch_bounds__(THREADS) void rrcdnet_short(const uint8_t* __restrict__ blob, const float* __restrict__ x,
-                                                         float* __restrict__ y, int L, int T, int tiles) {
+                                                         float* __restrict__ y, int L, int T, int tiles,
+                                                         unsigned* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
   if (!f16mix_blob_ok(blob)) return nan_outputs(tl, y, n, T);
   if (tl.base >= 0 && tl.base + TileGeo<2>::WB <= L) {
-    if (!hyb256::rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles)) rrcdnet_f16f8_tile<false, 2>(tl, y, n, L, T);
-  } else if (!hyb256::rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles)) {
-    rrcdnet_f16f8_tile<true, 2>(tl, y, n, L, T);
+    if (!hyb256::rrcdnet_hybrid_body<false, TAIL>(tl, blob, x, y, n, L, T, tiles, status))
+      rrcdnet_f16f8_tile<false, 2>(tl, y, n, L, T, status);
+  } else if (!hyb256::rrcdnet_hybrid_body<true, TAIL>(tl, blob, x, y, n, L, T, tiles, status)) {
+    rrcdnet_f16f8_tile<true, 2>(tl, y, n, L, T, status);
   }
 }
 
 #define IP_KERNEL(name, arch)                                                                              \
   template <int MODE, int TAIL = 0>                                                                         \
   __global__ __launch_bounds__(THREADS) void name(const uint8_t* __restrict__ blob, const float* __restrict__ x, \
-                                                 float* __restrict__ y, int L, int T, int tiles) {          \
+                                                 float* __restrict__ y, int L, int T, int tiles,            \
+                                                 unsigned* __restrict__ status) {                           \
     extern __shared__ __attribute__((aligned(16))) char lds[];                                             \
     int n;                                                                                                 \
     Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(arch), n);                                   \
     if (RDN_IP_PRIO && __builtin_amdgcn_readfirstlane(__builtin_amdgcn_workitem_id_x()) >= 256) __builtin_amdgcn_s_setprio(1);  \
     constexpr int NBK = NetGeo<arch>::NBK;                                                                 \
     const int need = L - tl.base + 2;  /* rows up to position L + 1: short last tiles */                     \
-    if (tl.base >= 0 && tl.base + TileGeo<NBK>::WB <= L) name##_body<MODE, false, NBK, TAIL>(tl, y, n, L, T);   \
-    else if (NBK == 5 && need <= 256) name##_body<MODE, true, NBK == 5 ? 2 : NBK, TAIL>(tl, y, n, L, T);          \
-    else if (NBK == 5 && need <= 384) name##_body<MODE, true, NBK == 5 ? 3 : NBK, TAIL>(tl, y, n, L, T);          \
-    else if (NBK == 5 && need <= 512) name##_body<MODE, true, NBK == 5 ? 4 : NBK, TAIL>(tl, y, n, L, T);          \
-    else name##_body<MODE, true, NBK, TAIL>(tl, y, n, L, T);                                                     \
+    if (tl.base >= 0 && tl.base + TileGeo<NBK>::WB <= L) name##_body<MODE, false, NBK, TAIL>(tl, y, n, L, T, status); \
+    else if (NBK == 5 && need <= 256) name##_body<MODE, true, NBK == 5 ? 2 : NBK, TAIL>(tl, y, n, L, T, status);  \
+    else if (NBK == 5 && need <= 384) name##_body<MODE, true, NBK == 5 ? 3 : NBK, TAIL>(tl, y, n, L, T, status);  \
+    else if (NBK == 5 && need <= 512) name##_body<MODE, true, NBK == 5 ? 4 : NBK, TAIL>(tl, y, n, L, T, status);  \
+    else name##_body<MODE, true, NBK, TAIL>(tl, y, n, L, T, status);                                             \
   }
 
 IP_KERNEL(denoisecnn, DENOISECNN)
@@ -322,7 +339,7 @@ IP_KERNEL(pidn, PIDN)
 #else
 #define RDN_F16MIX_KERNEL ip::rrcdnet<ip::MODE_H8, ip::RRCDNET_F16MIX_TAIL>
 #endif
-typedef void (*fused_kernel_t)(const uint8_t*, const float*, float*, int, int, int);
+typedef void (*fused_kernel_t)(const uint8_t*, const float*, float*, int, int, int, unsigned*);
 
 template <int MODE>
 static fused_kernel_t pick(int arch) {
@@ -337,7 +354,7 @@ static fused_kernel_t pick(int arch) {
 
 // RDN_F16MIX RRCDNet with 256-row tiles (ip::rrcdnet_short)
 hipError_t launch_fused_inplace_short(const uint8_t* blob, const float* x, float* y, int64_t n, int L,
-                                      hipStream_t stream) {
+                                      unsigned* status, hipStream_t stream) {
   const fused_kernel_t k = ip::rrcdnet_short<ip::RRCDNET_F16MIX_TAIL>;
   const hipError_t e = ensure_dynamic_lds((const void*)k, 92, (int)ip::TileGeo<2>::LDS, stream_device(stream));
   if (e != hipSuccess) return e;
@@ -346,14 +363,15 @@ hipError_t launch_fused_inplace_short(const uint8_t* blob, const float* x, float
   for (int64_t n0 = 0; n0 < n; n0 += chunk) {
     const int64_t nn = n - n0 < chunk ? n - n0 : chunk;
     hipLaunchKernelGGL(k, dim3((unsigned)(nn * tiles)), dim3(THREADS), ip::TileGeo<2>::LDS, stream, blob, x + n0 * L,
-                       y + n0 * L, L, T, tiles);
+                       y + n0 * L, L, T, tiles, status);
   }
   return hipGetLastError();
 }
 
 // dtype: F32 (exact fp32), BF16X3 (split bf16) or F16F8 (f16 + e4m3 correction); see common.hpp
+// status: the workspace's range word (RDN_F16F8 / RDN_F16MIX; NULL: a saturated tile's NaN outputs only)
 hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
-                                hipStream_t stream) {
+                                unsigned* status, hipStream_t stream) {
   if (arch < 0 || arch >= 8 || dtype < 0 || dtype > F16MIX) return hipErrorInvalidValue;
   const fused_kernel_t k = dtype == BF16X3 ? pick<ip::MODE_X3>(arch)
                            : dtype == F16F8 ? pick<ip::MODE_H8>(arch)
@@ -372,7 +390,7 @@ hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const 
   for (int64_t n0 = 0; n0 < n; n0 += chunk) {
     const int64_t nn = n - n0 < chunk ? n - n0 : chunk;
     hipLaunchKernelGGL(k, dim3((unsigned)(nn * tiles)), dim3(THREADS), lds, stream, blob, x + n0 * L,
-                       y + n0 * L, L, T, tiles);
+                       y + n0 * L, L, T, tiles, status);
   }
   return hipGetLastError();
 }

@@ -69,6 +69,7 @@ struct Tile {
   int layer;
   const float* small;
   uint64_t corr;        // MODE_H8: bit i = big layer i consumes the e4m3 correction (CORR_SLOT)
+  float amax;           // MODE_H8: running max of the values h8_sat saw (range guard, h8_track)
 };
 
 __device__ __forceinline__ bool in_range(int p, int L) { return p >= 0 && p < L; }
@@ -106,7 +107,7 @@ template <> struct Op<MODE_F32> {
   __device__ static B load_b_at(const char* act, const uint32_t (&ad)[PLANES], uint32_t off) {
     return B{*(const f32x4*)(act + ad[0] + off)};
   }
-  __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v) {
+  __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v, float* = nullptr) {
     *(f32x4*)(act + ad[0] + off) = v;
   }
   __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc, uint32_t, int) {
@@ -115,7 +116,9 @@ template <> struct Op<MODE_F32> {
     return acc;
   }
   // 4 channels [c0, c0+4) of a row
-  __device__ static void store4(char* act, int prow, int c0, f32x4 v) { *(f32x4*)(act + off_f32(prow, 4 * c0)) = v; }
+  __device__ static void store4(char* act, int prow, int c0, f32x4 v, float* = nullptr) {
+    *(f32x4*)(act + off_f32(prow, 4 * c0)) = v;
+  }
   __device__ static f32x4 load4(const char* act, int prow, int c0) { return *(const f32x4*)(act + off_f32(prow, 4 * c0)); }
 };
 
@@ -142,7 +145,7 @@ template <> struct Op<MODE_X3> {
   __device__ static B load_b_at(const char* act, const uint32_t (&ad)[PLANES], uint32_t off) {
     return B{*(const bf16x8*)(act + ad[0] + off), *(const bf16x8*)(act + ad[1] + off)};
   }
-  __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v) {
+  __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v, float* = nullptr) {
     const bf16x4 hi = __builtin_convertvector(v, bf16x4);           // 2 x v_cvt_pk_bf16_f32 (RNE)
     // hi back to f32 straight from the packed bits (one shift / mask each, no re-conversion)
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -158,7 +161,7 @@ template <> struct Op<MODE_X3> {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, acc, 0, 0, 0);
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, acc, 0, 0, 0);
   }
-  __device__ static void store4(char* act, int prow, int c0, f32x4 v) {
+  __device__ static void store4(char* act, int prow, int c0, f32x4 v, float* = nullptr) {
     const bf16x4 hi = __builtin_convertvector(v, bf16x4);           // 2 x v_cvt_pk_bf16_f32
     const bf16x4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x4), bf16x4);
     *(bf16x4*)(act + off_f32(prow, 2 * c0)) = hi;
@@ -205,13 +208,13 @@ template <typename E> struct OpS16 {
   __device__ static B load_b_at(const char* act, const uint32_t (&ad)[PLANES], uint32_t off) {
     return B{*(const V8*)(act + ad[0] + off)};
   }
-  __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v) {
+  __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v, float* = nullptr) {
     *(V4*)(act + ad[0] + off) = __builtin_convertvector(v, V4);
   }
   __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc, uint32_t, int) {
     return S16Types<E>::mma(a.hi, b.hi, acc);
   }
-  __device__ static void store4(char* act, int prow, int c0, f32x4 v) {
+  __device__ static void store4(char* act, int prow, int c0, f32x4 v, float* = nullptr) {
     *(V4*)(act + off_f32(prow, 2 * c0)) = __builtin_convertvector(v, V4);
   }
   __device__ static f32x4 load4(const char* act, int prow, int c0) {
@@ -267,6 +270,23 @@ __device__ __forceinline__ f32x4 h8_sat(f32x4 v) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_fmed3f(v[i], lo, H8_SAT);
   return v;
+}
+// Range guard of the e4m3 correction planes: h8_sat clamps |v| to H8_SAT, so every value it sees
+// first enters a per-lane running max (two v_max3 per 4 values; a rectified layer needs no |.|, its
+// negative values become 0).  The kernels vote the max at the end of a tile (range_vote): a tile
+// that saturated writes NaN outputs and raises the launch's status word (rdn_forward_status:
+// RDN_ERANGE) -- a clamped activation never reaches an output silently.
+template <bool RELU>
+__device__ __forceinline__ void h8_track(float& m, f32x4 v) {
+  // spelled as asm: the same maxima written with fmaxf made the compiler re-schedule the in-place
+  // epilogue into 56-350 VGPRs of spills (the f16f8 / hybrid kernels sit at 241-256 VGPRs)
+  if (RELU) {
+    asm("v_max3_f32 %0, %0, %1, %2" : "+v"(m) : "v"(v[0]), "v"(v[1]));
+    asm("v_max3_f32 %0, %0, %1, %2" : "+v"(m) : "v"(v[2]), "v"(v[3]));
+  } else {
+    asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(m) : "v"(v[0]), "v"(v[1]));
+    asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(m) : "v"(v[2]), "v"(v[3]));
+  }
 }
 // split a saturated activation into its three plane encodings
 struct H8Split {
@@ -346,14 +366,15 @@ template <> struct Op<MODE_H8> {
     for (int p = 0; p < PLANES; ++p) ad[p] = off_f32(prow, 16 * bslot(s, q, p));
     return load_b_at(act, ad, 0);
   }
-  __device__ static void put(char* act, uint32_t a0, uint32_t a1, uint32_t a2, f32x4 v) {
+  __device__ static void put(char* act, uint32_t a0, uint32_t a1, uint32_t a2, f32x4 v, float* amax) {
+    if (amax) h8_track<false>(*amax, v);
     const H8Split x = h8_split(h8_sat<false>(v));
     *(f16x4*)(act + a0) = x.hi;
     *(uint32_t*)(act + a1) = x.hi8;
     *(uint32_t*)(act + a2) = x.lo8;
   }
-  __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v) {
-    put(act, ad[0] + off, ad[1] + off, ad[2] + off, v);
+  __device__ static void store4_at(char* act, const uint32_t (&ad)[PLANES], uint32_t off, f32x4 v, float* amax = nullptr) {
+    put(act, ad[0] + off, ad[1] + off, ad[2] + off, v, amax);
   }
   __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc, uint32_t sa, int s) {
     const int sb = (__builtin_amdgcn_workitem_id_x() & 32) ? H8_LO_E8M0 : H8_HI_E8M0;   // lanes 32-63: the lo blocks
@@ -370,8 +391,8 @@ template <> struct Op<MODE_H8> {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[0], b.h[0], acc, 0, 0, 0);
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[1], b.h[1], acc, 0, 0, 0);
   }
-  __device__ static void store4(char* act, int prow, int c0, f32x4 v) {
-    put(act, off_f32(prow, sbyte(c0, 0)), off_f32(prow, sbyte(c0, 1)), off_f32(prow, sbyte(c0, 2)), v);
+  __device__ static void store4(char* act, int prow, int c0, f32x4 v, float* amax = nullptr) {
+    put(act, off_f32(prow, sbyte(c0, 0)), off_f32(prow, sbyte(c0, 1)), off_f32(prow, sbyte(c0, 2)), v, amax);
   }
   __device__ static f32x4 load4(const char* act, int prow, int c0) {
     const f16x4 h = *(const f16x4*)(act + off_f32(prow, sbyte(c0, 0)));
@@ -398,7 +419,7 @@ __device__ __forceinline__ const cfloat* small_slot(const Tile& tl, int slot) {
 // Conv1d(1, 64, 3, padding=1) (+ folded BN) + ReLU, one row per thread, fp32; ACCUM adds the
 // result onto the resident row (PIDN/train.py:105, identity recomputed from x).
 template <int MODE, bool ACCUM = false, int NBK = 4>
-__device__ __forceinline__ void stem(const Tile& tl, int slot) {
+__device__ __forceinline__ void stem(Tile& tl, int slot) {
   using TG = TileGeo<NBK>;
   const cfloat* sw = small_slot(tl, slot);
   for (int j = opaque_tid(); j < TG::WB; j += THREADS) {
@@ -422,7 +443,7 @@ __device__ __forceinline__ void stem(const Tile& tl, int slot) {
       if (ACCUM) a += v[i];
       v[i] = valid ? a : 0.f;
     }
-    Op<MODE>::store4(tl.lds, pr, 4 * cb, v);
+    Op<MODE>::store4(tl.lds, pr, 4 * cb, v, &tl.amax);
   }
   }
 }
@@ -759,6 +780,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
     for (int mm = 0; mm < MT; ++mm) {
       f32x4 v = res[j][i][mm];
       if (EPI & ADD_ID) v += id[(j * NT + i) * MT + mm];
+      h8_track<(EPI & RELU) != 0>(tl.amax, v);
       v = (EPI & RELU) ? h8_sat<true>(v) : h8_sat<false>(v);
       if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};
       if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
@@ -988,7 +1010,33 @@ __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const 
   tl.big = blob + SMALL_BYTES;
   tl.layer = 0;
   tl.corr = corr_mask(blob);
+  tl.amax = 0.f;
   return tl;
+}
+
+// End-of-tile range vote of the MODE_H8 kernels (h8_track): whether any lane of the workgroup saw a
+// value beyond H8_SAT.  Workgroup-uniform; one LDS word per wave at `vote_off`, which no wave may be
+// reading or about to write between the two barriers (callers pass a region their last phase is
+// done with).  A saturated tile raises *status (if given: the launch's workspace word, a relaxed
+// agent-scope vector store from one lane) and its caller writes NaN outputs.
+__device__ __forceinline__ bool range_vote(const Tile& tl, uint32_t vote_off, unsigned* status) {
+  unsigned* vote = (unsigned*)(tl.lds + vote_off);
+  const int tid = __builtin_amdgcn_workitem_id_x();
+  __syncthreads();
+  const bool wave_sat = __builtin_amdgcn_ballot_w64(tl.amax > H8_SAT) != 0;
+  if ((tid & 63) == 0) vote[tid >> 6] = wave_sat ? 1u : 0u;
+  __syncthreads();
+  bool sat = false;
+#pragma unroll
+  for (int k = 0; k < THREADS / 64; ++k) sat = sat || vote[k] != 0;
+  __syncthreads();
+  if (sat && status && tid == 0) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return sat;
+}
+template <int N>
+__device__ __forceinline__ void nan_rows(float (&o)[N]) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) o[k] = __uint_as_float(0x7fc00000u);
 }
 
 template <int MODE, int NBK = 4>

@@ -39,7 +39,10 @@ __device__ __forceinline__ void pingpong_to_tile(char* lds, uint32_t src) {
 struct H8Stage {
   f16x8 hi[PPNS::NT];
   uint32_t e_hi[PPNS::NT][2], e_lo[PPNS::NT][2];
+  float amax = 0.f;              // range guard (inplace.hpp h8_track): merged into the tile's after the layer
   __device__ __forceinline__ void put(int n, PPNS::f32x8 v) {
+    h8_track<true>(amax, __builtin_shufflevector(v, v, 0, 1, 2, 3));
+    h8_track<true>(amax, __builtin_shufflevector(v, v, 4, 5, 6, 7));
     const f32x4 a = h8_sat<true>(__builtin_shufflevector(v, v, 0, 1, 2, 3));
     const f32x4 b = h8_sat<true>(__builtin_shufflevector(v, v, 4, 5, 6, 7));
     const H8Split sa = h8_split(a), sb = h8_split(b);
@@ -70,7 +73,7 @@ struct H8Stage {
 // F16MIX_WIN_HI] (common.hpp): the caller then runs the all-corrected body on the tile.
 template <bool EDGE, int TAIL>
 __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blob, const float* x, float* y, int n,
-                                                    int L, int T, int tiles) {
+                                                    int L, int T, int tiles, unsigned* status) {
   constexpr int H = fused_halo(RRCDNET), NBK = HNBK, PP = 14 - TAIL;   // ping-pong layers of the right branch
   using HO = HeadOut<MODE_H8, NBK>;
   int n16;
@@ -88,10 +91,10 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
     bool spiked = false;
 #pragma unroll
     for (int k = 0; k < PPNS::WAVES; ++k) spiked = spiked || vote[k] != 0;
-    if (spiked) {
-      __syncthreads();             // every wave has read the votes before the fallback body writes
-      return false;
-    }
+    // every wave has read the votes before any wave writes again: the fallback body's stem, or layer
+    // 0's epilogue, whose last rows are the vote words
+    __syncthreads();
+    if (spiked) return false;
   }
   f32x4 id[16 * NBK / 4];
   LayerA<MODE_H8> a;
@@ -110,6 +113,7 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
       PPNS::layer<PPNS::STAGE, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1, false, nullptr, nullptr, &stg);
     }
     stg.write<EDGE>(tl.lds, t16);
+    tl.amax = fmaxf(tl.amax, stg.amax);
   }
   tl.layer = PP + 1;
   load_layer_a<MODE_H8>(tl, PP + 1, a);
@@ -162,7 +166,8 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
       if (j < PPNS::WB) lrow[j] = l[k];
     }
   }
-  PPNS::lds_barrier();
+  // the range vote of the corrected tail (its barriers also publish lrow); vote words behind lrow
+  const bool sat = range_vote(tl, PPNS::BUF1 + 4 * PPNS::WB, status);
   float o[HO::ROWS];
 #pragma unroll
   for (int k = 0; k < HO::ROWS; ++k) {      // x - (r + l)/2, one rounding
@@ -170,6 +175,7 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
     const float xv = in_range(p, L) ? tl.x[p] : 0.f;
     o[k] = (float)((double)xv - (parked_row<MODE_H8, NBK>(tl, y, n, k, H, T) + (double)lrow[HO::row(k)]) * 0.5);
   }
+  if (sat) nan_rows(o);
   store_out<MODE_H8, NBK>(tl, y, n, o, H, T);
   return true;
 }

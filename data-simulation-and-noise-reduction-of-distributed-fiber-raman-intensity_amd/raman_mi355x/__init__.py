@@ -7,6 +7,7 @@ Drop-in surfaces (reference file:line):
   evaluate, compute_*                             */evaulate.py:14-39 (evaluate.py, batched, on-device)
 """
 from . import engine
+from ._lib import EngineError, RangeError
 from .dataset import load_dataset, save_dataset
 from .distributed import all_reduce_sums, shard
 from .evaluate import evaluate, write_metrics
@@ -15,4 +16,4 @@ from .simulator import generate, generate_signals
 
 __all__ = ["engine", "DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN", "MODELS", "generate",
            "generate_signals", "evaluate", "write_metrics", "load_dataset", "save_dataset", "shard",
-           "all_reduce_sums"]
+           "all_reduce_sums", "EngineError", "RangeError"]

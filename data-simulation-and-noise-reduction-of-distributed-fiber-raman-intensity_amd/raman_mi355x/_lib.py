@@ -18,7 +18,7 @@ CSRC = os.path.join(os.path.dirname(PKG), "csrc")
 HEADER = os.path.join(os.path.dirname(os.path.dirname(PKG)), "include", "raman_mi355x.h")
 
 RDN_OK = 0
-ABI_VERSION = 3
+ABI_VERSION = 4
 # exact metric accumulator words (include/raman_mi355x.h RDN_ACC_*)
 ACC_LIMBS = 6
 ACC_STRIDE = ACC_LIMBS + 1
@@ -106,11 +106,19 @@ def lib():
     return _lib
 
 
+RDN_ERANGE = -6
+
+
 class EngineError(RuntimeError):
     pass
+
+
+class RangeError(EngineError):
+    """RDN_ERANGE: an RDN_F16F8 / RDN_F16MIX activation left the e4m3 correction planes' range (the
+    affected tiles' outputs are NaN); RDN_F32 / RDN_BF16X3 have no such bound."""
 
 
 def check(rc, what):
     if rc != RDN_OK:
         msg = lib().rdn_last_error().decode(errors="replace")
-        raise EngineError(f"{what} failed (code {rc}): {msg}")
+        raise (RangeError if rc == RDN_ERANGE else EngineError)(f"{what} failed (code {rc}): {msg}")

@@ -14,6 +14,9 @@ ARCHS = ("DenoiseCNN", "RRCDNet", "DSDN", "ADSDN", "PIDN", "APIDN")
 ARCH_ID = {a: i for i, a in enumerate(ARCHS)}
 CBAM_ARCHS = ("ADSDN", "APIDN")
 CBAM_IDS = tuple(ARCH_ID[a] for a in CBAM_ARCHS)
+# dtypes whose e4m3 correction planes bound the activations (|v| <= 1792): their forwards report a
+# saturated tile through the workspace's range word (RangeError) and write NaN for it
+RANGE_CODES = (3, 5)
 # Engine arithmetic modes (include/raman_mi355x.h rdn_dtype).  Every name here except
 # "bf16-unsafe" meets its north-star tolerance on every golden fixture (fp32: 1e-5 max-relative;
 # 16-bit modes: 2e-2 max-abs).  Single-rounding bf16 does NOT (0.24 on trained RRCDNet),
@@ -163,11 +166,19 @@ def _check_out(t, name, shape, device, dtype=torch.float32):
         raise ValueError(f"{name} must be contiguous")
 
 
+def needs_workspace(arch, code):
+    """A forward of (arch, code) takes a workspace: the CBAM team kernels (required) and the
+    range-checked dtypes (their range word)."""
+    return _arch(arch) in CBAM_IDS or code in RANGE_CODES
+
+
 class Workspace:
-    """Device scratch of the CBAM team kernels for (arch, dtype, L) on one device and stream, reused
-    across forwards.  Its hand-off error word is sticky: ``check()`` waits for the stream once and
-    raises EngineError if any forward since the last check timed out (rdn_forward_status), so a
-    batched driver checks once at the end instead of host-syncing every batch."""
+    """Device scratch of a forward for (arch, dtype, L) on one device and stream, reused across
+    forwards: the CBAM team kernels' slots and hand-off error word, and the range word of RDN_F16F8 /
+    RDN_F16MIX.  The status words are sticky: ``check()`` waits for the stream once and raises
+    EngineError if any forward since the last check timed out, RangeError if one saturated the e4m3
+    planes (rdn_forward_status), so a batched driver checks once at the end instead of host-syncing
+    every batch."""
 
     def __init__(self, arch, dtype, n, L, device, stream=None):
         self.arch, self.code, self.L = _arch(arch), resolve_dtype(arch, dtype), int(L)
@@ -189,7 +200,11 @@ class Workspace:
         return ctypes.c_void_p(self.buf.data_ptr() if self.buf is not None else 0)
 
     def fits(self, arch, code, n, L, device):
+        """Made for this network, dtype, length and device, large enough for n spectra, and bound to the
+        stream the forward launches on (torch's current stream): check() waits for self.stream only, and
+        rdn_workspace_init's reset is ordered on it."""
         return (self.arch, self.code, self.L, self.device) == (_arch(arch), code, int(L), torch.device(device)) \
+            and torch.cuda.current_stream(self.device).cuda_stream == self.stream.cuda_stream \
             and (self.n >= n or self.bytes_for(n) <= self.bytes)
 
     def bytes_for(self, n):
@@ -208,11 +223,13 @@ def forward(arch, dtype, packed, x, out=None, check=True, workspace=None):
     """y = Model(x) for x float32 (N, 1, L) (or (N, L)) on the GPU.
 
     ``dtype`` is an engine dtype name or ABI code (resolve_dtype).  The CBAM networks run one
-    team-persistent kernel whose workgroups hand off statistics.  With ``check`` (default) the call
-    waits for it and raises EngineError if a hand-off timed out (rdn_forward_status).  A batched
-    caller passes one ``Workspace`` to every forward with ``check=False`` and calls
-    ``workspace.check()`` once at the end (the error word is sticky); ``check=False`` without a
-    workspace keeps the launch asynchronous and unchecked (benchmarks: the affected outputs are NaN)."""
+    team-persistent kernel whose workgroups hand off statistics; RDN_F16F8 / RDN_F16MIX tiles whose
+    activations leave the e4m3 planes' range write NaN.  With ``check`` (default) the call waits for
+    the kernel and raises EngineError if a hand-off timed out, RangeError if a tile saturated
+    (rdn_forward_status).  A batched caller passes one ``Workspace`` to every forward with
+    ``check=False`` and calls ``workspace.check()`` once at the end (the status words are sticky);
+    ``check=False`` without a workspace keeps the launch asynchronous and unchecked (benchmarks: the
+    affected outputs are NaN)."""
     _check_cuda_f32(x, "input")
     if x.dim() == 3 and x.shape[1] != 1:
         raise ValueError(f"expected (N, 1, L) input, got {tuple(x.shape)}")
@@ -227,10 +244,10 @@ def forward(arch, dtype, packed, x, out=None, check=True, workspace=None):
     if y.data_ptr() < x.data_ptr() + x.numel() * 4 and x.data_ptr() < y.data_ptr() + y.numel() * 4:
         raise ValueError("out must not overlap the input (tiles re-read input halos while outputs are written)")
     ws = workspace
-    if ws is None and a in CBAM_IDS:
+    if ws is None and (a in CBAM_IDS or (check and code in RANGE_CODES)):
         ws = Workspace(a, code, n, L, x.device)
     elif ws is not None and not ws.fits(a, code, n, L, x.device):
-        raise ValueError("workspace was made for another network, dtype, length, device or a smaller batch")
+        raise ValueError("workspace was made for another network, dtype, length, device, stream or a smaller batch")
     L_ = _lib.lib()
     _lib.check(L_.rdn_forward(a, code, ctypes.c_void_p(packed.data_ptr()), ctypes.c_void_p(x.data_ptr()),
                               ctypes.c_void_p(y.data_ptr()), n, L,

@@ -58,14 +58,25 @@ def means_from_acc(acc):
     return {k: s[i] / s[4] for i, k in enumerate(KEYS)}
 
 
+def _engine_module(model):
+    """A raman_mi355x network whose own forward is the engine (not a subclass overriding forward)."""
+    from .models import _EngineNet
+    return isinstance(model, _EngineNet) and type(model).forward is _EngineNet.forward
+
+
 def _model_forward(model, x, ws):
-    """The module's forward without the per-call hand-off check (one Workspace.check at the end)."""
+    """The module's forward without the per-call hand-off check (one Workspace.check at the end);
+    any other nn.Module (or an engine module whose input the engine does not take) runs model(x), as
+    evaulate.py:30 does."""
+    if not (_engine_module(model) and model.uses_engine(x)):
+        return model(x)
     return engine.forward(model.ARCH, model.engine_code, model.packed_weights(x.device), x, check=False,
                           workspace=ws)
 
 
 def _workspace(model, n, L, device):
-    if model.ARCH not in engine.CBAM_ARCHS:
+    if (not _engine_module(model) or not engine.needs_workspace(model.ARCH, model.engine_code)
+            or torch.device(device).type != "cuda"):
         return None
     return engine.Workspace(model.ARCH, model.engine_code, n, L, device)
 
@@ -81,6 +92,9 @@ def evaluate(model, noisy_data, clean_data, batch_size=1024, device=None):
         raise ValueError(f"noisy {tuple(noisy.shape)} vs clean {tuple(clean.shape)}")
     lo, hi = shard(noisy.shape[0])
     L = noisy.shape[1]
+    if device.type != "cuda":
+        raise RuntimeError("raman_mi355x.evaluate runs its metrics on the GPU; on a CPU device use the module "
+                           "itself in the reference's evaulate.py loop (its forward falls back to eager PyTorch)")
     acc = engine.new_acc(device)
     ws = _workspace(model, min(batch_size, max(hi - lo, 1)), L, device)
     # fp64 clean stays fp64 (the metrics compare against the same float64 values as evaulate.py)

@@ -8,16 +8,22 @@ unchanged.  ``forward`` never executes the submodules: on first use (and after a
 change) the state_dict is folded/packed by the native library and the whole network runs as the
 fused gfx950 kernels of ``csrc/``.
 
-Supported: eval mode, CUDA float32 input ``(N, 1, L)``.  Training mode, CPU tensors and
-``requires_grad`` inputs raise (the engine is inference-only).
+The engine path: eval mode, CUDA float32 input ``(N, 1, L)``.  Everything the engine does not serve
+goes to the EAGER path, the reference forward written out on the same submodules (SURVEY.md §8(b)
+"fallback"): CPU tensors (an unchanged evaulate.py with ``DEVICE = "cpu"``, 1DCNN/evaulate.py:10),
+``module.training == True`` (BatchNorm batch statistics, running-stat updates: the train.py loops,
+RRCDNet/train.py:158-170) and inputs that require grad under autograd.  The eager path is plain
+PyTorch on whatever device the tensors are on; it never touches the native library.
 """
 import operator
+import warnings
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 from torch.nn import init
 
-from . import engine
+from . import _lib, engine
 
 # Registration generation: bumped whenever any module anywhere registers (or re-assigns) a parameter,
 # buffer or submodule (torch's global registration hooks), so the pack-cache below re-derives its
@@ -59,6 +65,9 @@ class _EngineNet(nn.Module):
         self._packed_key = None
         self._tensor_cache = None
         self._cache_gen = -1
+        self._ws = None                # status workspace of the range-checked / CBAM forwards
+        self._fp32 = None              # (key, blob) of the RDN_F32 re-run after a RangeError
+        self._range_warned = False
 
     # -- configuration -----------------------------------------------------------------------
     @property
@@ -74,8 +83,9 @@ class _EngineNet(nn.Module):
         """Arithmetic of the 64->64 convolutions:
         'fp32'        exact-fp32 MFMA with compensated accumulation: within 1e-5 of the fp32 reference;
         'f16'         one f16 MFMA per product, f16 activations, fp32 accumulation: the fastest mode
-                      within 2e-2.  On RRCDNet, where plain f16 misses the bar, the last three
-                      right-branch layers keep the e4m3 correction (RDN_F16MIX, 1.65e-2);
+                      within 2e-2.  On RRCDNet, where plain f16 misses the bar, the last five
+                      right-branch layers keep the e4m3 correction and tiles whose input leaves
+                      [-0.3, 1.3] run every layer corrected (RDN_F16MIX, DESIGN.md §4);
         'f16-plain'   plain f16 on every layer (RDN_F16) -- misses 2e-2 on trained RRCDNet (3.5e-2);
         'f16f8'       f16 product + one block-scaled e4m3 MFMA carrying both correction terms (~15
                       significant bits): within 2e-2 (measured <= 1e-3);
@@ -121,21 +131,53 @@ class _EngineNet(nn.Module):
             self._packed_key = key
         return self._packed
 
+    def _fp32_weights(self, device):
+        k = self._state_key(device)
+        key = (k[0],) + k[2:]
+        if self._fp32 is None or self._fp32[0] != key:
+            with torch.no_grad():
+                self._fp32 = (key, engine.pack(self.ARCH, self.state_dict(), 0, device))
+        return self._fp32[1]
+
+    def _workspace(self, x):
+        """The cached status workspace for this forward (None when the dtype and network need none)."""
+        code = self._engine_code
+        if not engine.needs_workspace(self.ARCH, code):
+            return None
+        n, L = x.shape[0], x.shape[-1]
+        if self._ws is None or not self._ws.fits(self.ARCH, code, n, L, x.device):
+            self._ws = engine.Workspace(self.ARCH, code, n, L, x.device)
+        return self._ws
+
     # -- forward -----------------------------------------------------------------------------
+    def uses_engine(self, x):
+        """Whether ``forward(x)`` runs the fused HIP kernels (True) or the eager reference forward:
+        eval mode, a CUDA tensor, and no autograd graph requested through the input."""
+        return (not self.training and torch.is_tensor(x) and x.is_cuda
+                and not (torch.is_grad_enabled() and x.requires_grad))
+
+    def eager_forward(self, x):
+        """The reference forward on this module's own submodules (plain PyTorch, any device)."""
+        raise NotImplementedError
+
     def forward(self, x):
-        if self.training:
-            raise RuntimeError(f"{type(self).__name__}: the raman_mi355x engine is inference-only; "
-                               "call model.eval() first (training is out of scope)")
-        if not (torch.is_tensor(x) and x.is_cuda):
-            raise RuntimeError(f"{type(self).__name__}: raman_mi355x runs on the GPU only; move the "
-                               "model input to a CUDA (HIP) device")
-        if torch.is_grad_enabled() and x.requires_grad:
-            raise RuntimeError(f"{type(self).__name__}: autograd is not supported by the engine")
+        if not self.uses_engine(x):
+            return self.eager_forward(x)
         if x.dim() != 3 or x.shape[1] != 1:
             raise ValueError(f"{type(self).__name__}: expected input (N, 1, L), got {tuple(x.shape)}")
         if x.dtype != torch.float32:
             raise TypeError(f"{type(self).__name__}: expected float32 input, got {x.dtype}")
-        return engine.forward(self.ARCH, self._engine_code, self.packed_weights(x.device), x)
+        try:
+            return engine.forward(self.ARCH, self._engine_code, self.packed_weights(x.device), x,
+                                  workspace=self._workspace(x))
+        except _lib.RangeError:
+            # an activation left the e4m3 planes' range (inputs far beyond normalised intensity):
+            # never return the NaN tiles -- the batch is re-run in exact fp32, which has no such bound
+            if not self._range_warned:
+                warnings.warn(f"{type(self).__name__}: activations beyond the '{self._engine_dtype}' range "
+                              "(|v| > 1792); this batch ran in fp32 instead", RuntimeWarning, stacklevel=2)
+                self._range_warned = True
+            return engine.forward(self.ARCH, 0, self._fp32_weights(x.device), x)
 
 
 def _check_defaults(name, in_channels, num_res_blocks):
@@ -153,6 +195,9 @@ class DenoiseCNN(_EngineNet):
         super().__init__()
         body = [_seq(_conv(), nn.ReLU()) for _ in range(18)]
         self.layers = _seq(_conv(1, C), nn.ReLU(), *body, _conv(C, 1))
+
+    def eager_forward(self, x):
+        return self.layers(x)                                        # 1DCNN/train.py:81-82
 
 
 class RRCDNet(_EngineNet):
@@ -178,6 +223,9 @@ class RRCDNet(_EngineNet):
                 init.ones_(mod.weight)
                 init.zeros_(mod.bias)
 
+    def eager_forward(self, x):
+        return x - (self.right_net(x) + self.left_net(x)) / 2      # RRCDNet/train.py:95-98
+
 
 class _ResidualBlock(nn.Module):
     """DSDN/ADSDN ResidualBlock parameter layout (conv1, bn1, conv2, bn2[, cbam])."""
@@ -189,6 +237,14 @@ class _ResidualBlock(nn.Module):
         if with_cbam:
             self.cbam = _CBAM(bias=True, names=("channel_attention", "spatial_attention"))
 
+    def forward(self, x):
+        # DSDN/train.py:93-98, ADSDN/train.py:133-139 (CBAM on the second BN's output)
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        if hasattr(self, "cbam"):
+            out = self.cbam(out)
+        return F.relu(out + x)
+
 
 class _Stem(nn.Module):
     """DownSampling parameter layout: ``conv`` (+ ``cbam`` in ADSDN)."""
@@ -199,6 +255,10 @@ class _Stem(nn.Module):
         if with_cbam:
             self.cbam = _CBAM(bias=True, names=("channel_attention", "spatial_attention"))
 
+    def forward(self, x):
+        x = F.relu(self.conv(x))                                     # DSDN/train.py:79-80
+        return self.cbam(x) if hasattr(self, "cbam") else x          # ADSDN/train.py:125-128
+
 
 class _ChannelAttention(nn.Module):
     def __init__(self, bias):
@@ -208,12 +268,23 @@ class _ChannelAttention(nn.Module):
         self.fc = _seq(nn.Linear(C, C // 16, bias=bias), nn.ReLU(inplace=True), nn.Linear(C // 16, C, bias=bias))
         self.sigmoid = nn.Sigmoid()
 
+    def forward(self, x):
+        # ADSDN/train.py:84-89: one MLP on the pooled mean and max, summed, sigmoid
+        b, c, _ = x.shape
+        out = self.fc(self.avg_pool(x).view(b, c)) + self.fc(self.max_pool(x).view(b, c))
+        return self.sigmoid(out).view(b, c, 1)
+
 
 class _SpatialAttention(nn.Module):
     def __init__(self, bias):
         super().__init__()
         self.conv = nn.Conv1d(2, 1, 7, padding=3, bias=bias)
         self.sigmoid = nn.Sigmoid()
+
+    def forward(self, x):
+        # ADSDN/train.py:99-104: channel mean and max -> Conv1d(2, 1, 7) -> sigmoid
+        pooled = torch.cat([torch.mean(x, dim=1, keepdim=True), torch.max(x, dim=1, keepdim=True)[0]], dim=1)
+        return self.sigmoid(self.conv(pooled))
 
 
 class _CBAM(nn.Module):
@@ -222,8 +293,13 @@ class _CBAM(nn.Module):
 
     def __init__(self, bias, names):
         super().__init__()
+        self._names = names
         setattr(self, names[0], _ChannelAttention(bias))
         setattr(self, names[1], _SpatialAttention(bias))
+
+    def forward(self, x):
+        x = x * getattr(self, self._names[0])(x)
+        return x * getattr(self, self._names[1])(x)
 
 
 class DSDN(_EngineNet):
@@ -239,6 +315,11 @@ class DSDN(_EngineNet):
         self.res_blocks = _seq(*[_ResidualBlock() for _ in range(num_res_blocks)])
         self.conv_out = _conv(C, in_channels)
 
+    def eager_forward(self, x):
+        # DSDN/train.py:120-126 (its extra relu on the stem's relu output is the identity)
+        x = F.relu(self.conv2(F.relu(self.conv1(F.relu(self.down_sampling(x))))))
+        return self.conv_out(self.res_blocks(x))
+
 
 class ADSDN(_EngineNet):
     """ADSDN/train.py:150-167."""
@@ -253,6 +334,11 @@ class ADSDN(_EngineNet):
         self.cbam = _CBAM(bias=True, names=("channel_attention", "spatial_attention"))
         self.res_blocks = _seq(*[_ResidualBlock(with_cbam=True) for _ in range(num_res_blocks)])
         self.conv_out = _conv(C, in_channels)
+
+    def eager_forward(self, x):
+        # ADSDN/train.py:160-167
+        x = F.relu(self.conv2(F.relu(self.conv1(self.down_sampling(x)))))
+        return self.conv_out(self.res_blocks(self.cbam(x)))
 
 
 def _pidn_block(cbam=False):
@@ -274,6 +360,10 @@ class PIDN(_EngineNet):
         self.res_blocks = _seq(*[_pidn_block() for _ in range(num_res_blocks)])
         self.conv_out = _seq(_conv(C, in_channels), nn.Sigmoid())
 
+    def eager_forward(self, x):
+        x = self.down_sampling(x)                                    # PIDN/train.py:101-106
+        return self.conv_out(self.res_blocks(x) + x)
+
 
 class APIDN(_EngineNet):
     """APIDN/train.py:119-159."""
@@ -286,6 +376,13 @@ class APIDN(_EngineNet):
         self.down_sampling = _seq(_conv(in_channels, C), nn.ReLU())
         self.res_blocks = nn.ModuleList([_pidn_block(cbam=True) for _ in range(num_res_blocks)])
         self.conv_out = _seq(_conv(C, in_channels), nn.Sigmoid())
+
+    def eager_forward(self, x):
+        x = self.down_sampling(x)                                    # APIDN/train.py:151-159
+        identity = x
+        for block in self.res_blocks:
+            x = x + block(x)
+        return self.conv_out(x + identity)
 
 
 MODELS = {cls.ARCH: cls for cls in (DenoiseCNN, RRCDNet, DSDN, ADSDN, PIDN, APIDN)}

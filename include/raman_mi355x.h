@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RDN_ABI_VERSION 3
+#define RDN_ABI_VERSION 4
 
 typedef enum {
   RDN_DENOISECNN = 0, /* 1DCNN/train.py   class DenoiseCNN */
@@ -55,7 +55,11 @@ typedef enum {
  *   RDN_F16F8  f16 main product (v = hi + lo, hi = f16(v)) plus both correction products
  *              W_lo*X_hi + W_hi*X_lo as ONE block-scaled e4m3 MFMA at twice the 16-bit rate; f16 hi
  *              + e4m3 lo activations (~15 significant bits).  2e-2-safe at 2/3 of the MFMA cycles
- *              of RDN_BF16X3.  Activations saturate at +-1792 (the e4m3 range of hi / 4).
+ *              of RDN_BF16X3.  Range: the e4m3 planes hold |activation| <= 1792 (hi / 4 in e4m3); a
+ *              tile whose activations exceed it writes NaN outputs and raises the workspace's range
+ *              word (rdn_forward_status: RDN_ERANGE) -- never a silently clamped value.  Inputs of
+ *              normalised intensity stay far inside it (trained networks: max |activation| 9-28);
+ *              ~100x larger inputs need RDN_F32 or RDN_BF16X3.
  *   RDN_F16    one f16 MFMA per product (v_mfma_f32_16x16x32_f16, the bf16 rate), f16 weights and
  *              activations (11 significant bits), fp32 accumulation: the fastest mode within the 2e-2
  *              bf16 bar on the golden fixtures of 1DCNN, DSDN, ADSDN, PIDN and APIDN (worst 6.9e-3,
@@ -66,7 +70,8 @@ typedef enum {
  *              layers of the right branch (the ones the head's cancellation x - (r + l)/2 amplifies),
  *              and every layer corrected on a tile whose input window leaves [-0.3, 1.3] (a spike):
  *              within 2e-2 (1.19e-2 on the trained fixture, 1.54e-2 worst over config 1's 1000
- *              spectra).  One hybrid kernel: the plain layers, the whole left branch and its head
+ *              spectra).  The corrected layers have RDN_F16F8's range and range guard (RDN_ERANGE).
+ *              One hybrid kernel: the plain layers, the whole left branch and its head
  *              on the RDN_F16 ping-pong engine, the corrected tail and the right head on the in-place
  *              tile.  The corrected layers are compiled in; rdn_get_correction_mask reads them back
  *              from a packed blob.
@@ -81,7 +86,9 @@ enum {
   RDN_EUNSUPPORTED = -2, /* combination not built                                            */
   RDN_ESHAPE = -3,       /* a tensor handed to rdn_pack has the wrong number of elements      */
   RDN_ESIZE = -4,        /* destination / workspace buffer too small                          */
-  RDN_EHIP = -5          /* a HIP runtime call failed (message carries hipGetErrorString)     */
+  RDN_EHIP = -5,         /* a HIP runtime call failed (message carries hipGetErrorString)     */
+  RDN_ERANGE = -6        /* rdn_forward_status: an RDN_F16F8 / RDN_F16MIX activation left the
+                            e4m3 planes' range; the affected tiles' outputs are NaN          */
 };
 
 /* ABI version (RDN_ABI_VERSION) of the loaded library. */
@@ -122,13 +129,16 @@ int rdn_check_blob(int arch, int dtype, const void* host_blob, size_t bytes);
 int rdn_default_correction_mask(int arch, uint64_t* mask);
 int rdn_get_correction_mask(int arch, int dtype, const void* host_blob, size_t bytes, uint64_t* mask);
 
-/* Device scratch rdn_forward needs for a batch on the device of `stream` (0 for the fully fused
- * networks; the CBAM team geometry depends on the device's CU count and occupancy). */
+/* Device scratch rdn_forward takes for a batch on the device of `stream`: the CBAM networks' team
+ * geometry (depends on the device's CU count and occupancy; required), RDN_F16F8 / RDN_F16MIX on the
+ * fused networks 256 bytes for the range word (optional: without it a saturated tile's outputs are
+ * still NaN, but rdn_forward_status cannot report it), 0 otherwise. */
 int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes, void* stream);
 
-/* Prepare a newly allocated workspace for rdn_forward on `stream`: clears its hand-off error word
- * (the word is sticky across forwards until rdn_forward_status reads and clears it, so one status
- * call after many forwards that share a workspace covers all of them). */
+/* Prepare a newly allocated workspace for rdn_forward on `stream`: clears its status words -- the
+ * CBAM hand-off error word and the range word (both sticky across forwards until rdn_forward_status
+ * reads and clears them, so one status call after many forwards that share a workspace covers all
+ * of them). */
 int rdn_workspace_init(int arch, int dtype, int64_t n, int64_t L, void* workspace, size_t workspace_bytes,
                        void* stream);
 
@@ -139,13 +149,16 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
                 void* workspace, size_t workspace_bytes, void* stream);
 
 /* Completion status of every rdn_forward enqueued on `stream` with this workspace since the last
- * status call (or rdn_workspace_init): waits for the stream (hipStreamSynchronize), then, for the
- * CBAM networks (ADSDN, APIDN), reads and clears the team kernel's sticky hand-off error word.
- * RDN_EHIP if a team wait timed out (co-residency broken by a concurrent kernel; the affected
- * spectra's outputs are NaN) or the stream reported an error; RDN_ESIZE if the workspace is smaller
- * than this device's team geometry needs; RDN_OK otherwise.  Replaces nothing in the reference (its
- * forward is synchronous PyTorch): the Python module calls it after each CBAM forward of the
- * evaulate.py loop, the batched evaluate drivers once at the end. */
+ * status call (or rdn_workspace_init): waits for the stream (hipStreamSynchronize), then reads and
+ * clears the workspace's sticky status words.  RDN_EHIP if a CBAM team wait timed out (co-residency
+ * broken by a concurrent kernel; the affected spectra's outputs are NaN) or the stream reported an
+ * error; RDN_ERANGE if an RDN_F16F8 / RDN_F16MIX activation left the e4m3 planes' range (NaN tiles;
+ * for the CBAM networks the CBAM statistics of the saturated tile also reached the rest of its
+ * spectrum, so the status word, not the NaN, is the authoritative signal); RDN_ESIZE if the workspace
+ * is smaller than this device's team geometry needs; RDN_OK otherwise.  Replaces nothing in the
+ * reference (its forward is synchronous PyTorch): the Python module calls it after each
+ * range-checked or CBAM forward (and re-runs a saturated batch in RDN_F32), the batched evaluate
+ * drivers once at the end. */
 int rdn_forward_status(int arch, int dtype, int64_t n, int64_t L, void* workspace, size_t workspace_bytes,
                        void* stream);
 

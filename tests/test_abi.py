@@ -27,7 +27,7 @@ def test_exports_every_declared_symbol(lib):
     assert declared == set(_lib.EXPORTED), declared ^ set(_lib.EXPORTED)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.rdn_version() == 3
+    assert lib.rdn_version() == 4
 
 
 def test_library_built_from_these_sources(lib):
@@ -65,6 +65,23 @@ def test_every_f16_spelling_selects_the_same_arithmetic(spelling):
     assert engine.packed_size("RRCDNet", spelling) == engine.packed_size("RRCDNet", "f16mix")
     with pytest.raises(ValueError, match="resolves per network"):
         engine._dtype(spelling)
+
+
+def test_range_checked_dtypes_take_a_status_workspace(lib):
+    """ABI v4: RDN_F16F8 / RDN_F16MIX on the fused networks report a saturated e4m3 plane through a
+    256-byte workspace word (rdn_forward_status: RDN_ERANGE = -6); the other fused modes need none,
+    and rdn_workspace_init refuses a too-small range workspace (no GPU call is made for these)."""
+    from raman_mi355x import _lib, engine
+    n = ctypes.c_size_t()
+    for arch in (0, 1, 2, 4):
+        for code, need in ((0, 0), (2, 0), (4, 0), (1, 0), (3, 256)):
+            assert lib.rdn_workspace_size(arch, code, 8, 1000, ctypes.byref(n), None) == 0
+            assert n.value == need, (arch, code, n.value)
+            assert engine.needs_workspace(arch, code) == (need > 0)
+    assert lib.rdn_workspace_size(1, 5, 8, 1000, ctypes.byref(n), None) == 0 and n.value == 256
+    assert lib.rdn_workspace_init(1, 5, 8, 1000, None, 0, None) == -4
+    assert lib.rdn_workspace_init(0, 0, 8, 1000, None, 0, None) == 0
+    assert _lib.RDN_ERANGE == -6 and issubclass(_lib.RangeError, _lib.EngineError)
 
 
 def test_f16mix_is_refused_for_other_networks_before_dispatch(lib):

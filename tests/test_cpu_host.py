@@ -3,6 +3,7 @@ dataset format, sharding, and the world_size-2 metric all-reduce over gloo."""
 import json
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -75,15 +76,51 @@ def test_module_state_dict_is_reference_compatible(arch):
     m.load_state_dict(golden_state_dict(arch, "synth"), strict=True)
 
 
-def test_module_refuses_cpu_and_training():
+def test_module_unsupported_configuration_raises():
     import raman_mi355x as R
-    m = R.PIDN()
-    with pytest.raises(RuntimeError, match="inference-only"):
-        m.train()(torch.zeros(1, 1, 16))
-    with pytest.raises(RuntimeError, match="GPU only"):
-        m.eval()(torch.zeros(1, 1, 16))
     with pytest.raises(NotImplementedError):
         R.DSDN(num_res_blocks=3)
+
+
+@pytest.mark.parametrize("arch", ARCHS)
+def test_eager_fallback_matches_reference_goldens(arch, inputs):
+    """SURVEY.md §8(b) fallback: a CPU tensor runs the reference forward on the module's own
+    submodules (an unchanged evaulate.py with DEVICE = "cpu", 1DCNN/evaulate.py:10): the golden
+    checkpoints load strictly and reproduce the reference's fp32 CPU outputs within 1e-6."""
+    import raman_mi355x as R
+    g = load_golden(arch)
+    whichs = ["synth"] + (["trained"] if any(k.startswith("w::") for k in g.files) else [])
+    for which in whichs:
+        m = R.MODELS[arch]()
+        m.load_state_dict(golden_state_dict(arch, which), strict=True)
+        m.eval()
+        assert not m.uses_engine(torch.zeros(1, 1, 8))
+        for name in ("main", "edge33", "edge7"):
+            x = torch.from_numpy(input_array(inputs, name)).unsqueeze(1)
+            with torch.no_grad():
+                y = m(x).squeeze(1).numpy()
+            ref = g[f"{which}_{name}"]
+            assert np.abs(y - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max()), (arch, which, name)
+
+
+def test_eager_fallback_trains():
+    """Training mode and requires_grad inputs take the eager path: BatchNorm uses batch statistics and
+    updates its running stats, and gradients reach every parameter (RRCDNet/train.py:158-170)."""
+    import raman_mi355x as R
+    torch.manual_seed(0)
+    m = R.RRCDNet().train()
+    x = torch.rand(2, 1, 64)
+    assert not m.uses_engine(x)
+    rm0 = m.right_net[1].running_mean.clone()
+    loss = torch.nn.functional.mse_loss(m(x), x)
+    loss.backward()
+    assert not torch.equal(m.right_net[1].running_mean, rm0)
+    assert all(p.grad is not None for p in m.parameters())
+    m.eval()
+    xg = torch.rand(1, 1, 32, requires_grad=True)
+    assert not m.uses_engine(xg)
+    m(xg).sum().backward()
+    assert xg.grad is not None
 
 
 def test_checkpoint_round_trip(tmp_path):
@@ -166,6 +203,52 @@ def test_bench_algorithmic_flops_match_survey():
         assert abs(bench.flops_per_spectrum(arch, 10000) - g) / g < 5e-5, arch
     assert abs(bench.flops_per_spectrum("PIDN", 16384) - 12.092e9) / 12.092e9 < 5e-4
     assert abs(bench.flops_per_spectrum("APIDN", 16384) - 12.099e9) / 12.099e9 < 5e-4
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    return bench
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_bench_index_blocks_disjoint(world):
+    """bench.py's legs never re-generate each other's spectra: every rank's headline batch, pipeline
+    batches and config-4 shard (evaluate_synthetic: [first + r N/W, first + (r+1) N/W)), and the config-4
+    warm-up, are pairwise disjoint simulator index ranges for W = 1, 2, 8."""
+    from raman_mi355x.distributed import shard
+    bench = _bench_module()
+    B, B4, chunks = 8192, 8192, 4
+    ranges = []
+    for r in range(world):
+        b = bench.index_blocks(world, r, B, 3, B4, chunks)
+        ranges += [b["headline"], b["pipeline"]]
+        lo, hi = shard(b["config4_total"], r, world)
+        ranges.append((b["config4_first"] + lo, b["config4_first"] + hi))
+    ranges.append((b["config4_warmup_first"], b["config4_warmup_first"] + 2 * world))
+    ranges.sort()
+    assert all(a[1] <= c[0] for a, c in zip(ranges, ranges[1:])), ranges
+    assert ranges[0][0] == 0
+
+
+def test_bench_gpus_flag_launches_ranks(monkeypatch):
+    """`python bench.py --gpus N` without torchrun starts N ranks under torch.distributed.run (before any
+    GPU call), forwarding its arguments; with WORLD_SIZE set (a launched rank) it does not re-launch."""
+    bench = _bench_module()
+    calls = []
+    monkeypatch.setattr("subprocess.call", lambda cmd: calls.append(cmd) or 0)
+    assert bench.launch_ranks(4, ["--gpus", "4", "--dist-backend", "gloo"]) == 0
+    cmd = calls[0]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and cmd[-4:] == ["--gpus", "4", "--dist-backend", "gloo"]
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "launch_ranks", lambda n, argv: calls.append(("launch", n)) or 7)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "3", "--dist-backend", "gloo"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 7 and calls[-1] == ("launch", 3)
 
 
 def test_refgen_reproduces_reference_generator_bit_exact(inputs):

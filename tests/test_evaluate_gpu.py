@@ -90,3 +90,39 @@ def test_evaluate_matches_skimage_golden(tmp_path, inputs):
     ref = g["per_spectrum"][:3].mean(axis=0)
     for i, k in enumerate(("MSE", "SSIM", "Smoothness", "Peak2Peak")):
         assert abs(got[k] - ref[i]) <= 1e-5 * abs(ref[i]), (k, got[k], ref[i])
+
+
+def test_evaluate_accepts_any_module(tmp_path, inputs):
+    """evaluate() takes any nn.Module as evaulate.py:25-39 does: a plain PyTorch module (here the engine
+    module's eager forward wrapped in another module) runs model(x) per batch; the device metrics then
+    agree with the engine module's own evaluation to the fp32 forward's difference."""
+    from raman_mi355x.evaluate import evaluate
+    m = _module("RRCDNet", "trained", "fp32", tmp_path)
+
+    class Plain(torch.nn.Module):
+        def __init__(self, inner):
+            super().__init__()
+            self.inner = inner
+
+        def forward(self, x):
+            return self.inner.eager_forward(x)
+
+    a = evaluate(Plain(m), inputs["main_noisy"], inputs["main_clean64"], batch_size=2)
+    b = evaluate(m, inputs["main_noisy"], inputs["main_clean64"], batch_size=2)
+    for k in a:
+        assert abs(a[k] - b[k]) <= 1e-5 * abs(b[k]), (k, a[k], b[k])
+
+
+def test_workspace_is_bound_to_its_stream():
+    """A CBAM Workspace made on one stream is refused on another (its check() waits for its own stream)."""
+    import raman_mi355x as R
+    from raman_mi355x import engine
+    m = R.ADSDN().cuda().eval().set_engine_dtype("f16")
+    x = torch.rand(2, 1, 700, device="cuda")
+    ws = engine.Workspace("ADSDN", m.engine_code, 2, 700, x.device)
+    engine.forward("ADSDN", m.engine_code, m.packed_weights(x.device), x, workspace=ws)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with pytest.raises(ValueError, match="stream"):
+            engine.forward("ADSDN", m.engine_code, m.packed_weights(x.device), x, workspace=ws)
+    torch.cuda.synchronize()

@@ -70,7 +70,7 @@ def test_pipeline_matches_oracle(dtype):
     ref = oracle_forward(arch, golden_state_dict(arch, "trained"), torch.from_numpy(x).unsqueeze(1)).squeeze(1).numpy()
     scale = max(np.abs(ref).max(), 1e-30)
     err = np.abs(y - ref).max()
-    tol = 1e-5 * scale if dtype == "fp32" else 2e-2 * max(1.0, scale)
+    tol = 1e-5 * scale if dtype == "fp32" else 2e-2          # trained weights: the plain 2e-2 max-abs bar
     assert err <= tol, f"{dtype}: {err:.3e} > {tol:.3e}"
     # metric sums of the pipeline vs the oracle's metrics on the pipeline's own outputs
     clean, _, _, _ = engine.generate(4, SEED, first_index=1000, signal_length=L, device="cuda")
