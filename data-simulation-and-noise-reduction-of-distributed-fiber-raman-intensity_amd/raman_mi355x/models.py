@@ -140,9 +140,11 @@ class _EngineNet(nn.Module):
         return self._fp32[1]
 
     def _workspace(self, x):
-        """The cached status workspace for this forward (None when the dtype and network need none)."""
+        """The cached range-status workspace of an RDN_F16F8 / RDN_F16MIX forward on a fused network
+        (256 bytes, one layout).  None otherwise: a CBAM network's team workspace depends on the device
+        geometry and the segment switch, so engine.forward makes one per call (caching allocator)."""
         code = self._engine_code
-        if not engine.needs_workspace(self.ARCH, code):
+        if self.ARCH in engine.CBAM_ARCHS or code not in engine.RANGE_CODES:
             return None
         n, L = x.shape[0], x.shape[-1]
         if self._ws is None or not self._ws.fits(self.ARCH, code, n, L, x.device):

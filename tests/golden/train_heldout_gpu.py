@@ -75,8 +75,9 @@ def main():
         opt.load_state_dict(st["opt"])
         step, best, losses, pos = st["step"], st["best"], st["losses"], st["pos"]
         perm = st["perm"]
-        gen.set_state(st["gen"])
-        best_sd = st["best_sd"]
+        gen.set_state(st["gen"].cpu())
+        perm = perm.cpu()
+        best_sd = {k: v.cpu() for k, v in st["best_sd"].items()} if st["best_sd"] is not None else None
         print(f"resumed at step {step}, best val {best:.6f}", flush=True)
 
     def validate():

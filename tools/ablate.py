@@ -34,7 +34,8 @@ VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "saglobal": "-DRDN_T16_SA_LOCAL=0", "untag_saglobal": "-DRDN_T16_TAGGED=0 -DRDN_T16_SA_LOCAL=0", "salocal": "-DRDN_T16_SA_LOCAL=1", "pf2": "-DRDN_H16_PF=2", "pf4": "-DRDN_H16_PF=4", "edgesel": "-DRDN_H16_EDGE_POST=0", "alledge": "-DRDN_ABLATE_ALLEDGE -DRDN_TEAM_STAMPS=1",
             "tail3": "-DRDN_F16MIX_TAIL=3", "tail4": "-DRDN_F16MIX_TAIL=4", "tail5": "-DRDN_F16MIX_TAIL=5",
             "r02": "-DRDN_T16_TAGGED=0 -DRDN_T16_SA_LOCAL=0 -DRDN_TEAM_STAMPS=1",
-            "meanvalu": "-DRDN_T16_MEAN_MFMA=0", "sa1": "-DRDN_T16_SA_PAIR=0", "nostage": "-DRDN_F16MIX_STAGE=0", "nowin": "-DRDN_F16MIX_WIN=0", "mlp0": "-DRDN_T16_MLP_BFLY=0", "per2": "-DRDN_T16_POLL_PER=2", "sleep0": "-DRDN_TEAM_SLEEP=0", "sleep1": "-DRDN_TEAM_SLEEP=1", "sleep4": "-DRDN_TEAM_SLEEP=4", "nostem": "-DRDN_ABLATE_NOSTEM", "stem1": "-DRDN_H16_STEM2=0", "stem2a": "-DRDN_H16_STEM2=1", "noheadv": "-DRDN_ABLATE_NOHEADV"}
+            "meanvalu": "-DRDN_T16_MEAN_MFMA=0", "sa1": "-DRDN_T16_SA_PAIR=0", "nostage": "-DRDN_F16MIX_STAGE=0", "nowin": "-DRDN_F16MIX_WIN=0", "mlp0": "-DRDN_T16_MLP_BFLY=0", "per2": "-DRDN_T16_POLL_PER=2", "sleep0": "-DRDN_TEAM_SLEEP=0", "sleep1": "-DRDN_TEAM_SLEEP=1", "sleep4": "-DRDN_TEAM_SLEEP=4", "nostem": "-DRDN_ABLATE_NOSTEM", "stem1": "-DRDN_H16_STEM2=0", "stem2a": "-DRDN_H16_STEM2=1", "noheadv": "-DRDN_ABLATE_NOHEADV",
+            "tail0": "-DRDN_F16MIX_TAIL=0", "tail2": "-DRDN_F16MIX_TAIL=2"}
 
 
 def build():
