@@ -341,7 +341,7 @@ struct TeamArgs {
   unsigned* err;         // hand-off error words: [0] this launch (fast-fail, NaN outputs), [1] sticky (cbam_status)
   unsigned long long* stamps;   // RDN_TEAM_STAMPS diagnostics: [grid][NSTAMP] cycle sums per phase
   int force_miss;       // test knob (RDN_CBAM_FORCE_MISS=k): workgroup 0 skips its k-th arrival
-  int xcd;              // team16: 1 = same-XCD teams may hand off through their XCD's L2 (RDN_T16_XCD)
+  int xcd;              // team16: 1 = same-XCD teams may hand off through their XCD's L2
   unsigned tag0;        // team16: this launch's first granule tag - 1 (tags never repeat across launches)
 };
 #ifndef RDN_TEAM_STAMPS
@@ -573,17 +573,10 @@ __device__ __forceinline__ void team_wait(const TeamArgs& ta, unsigned* ctr, uns
 // APIDN/train.py:113-116,154-156), written over u (and, with save_next, as the next block's
 // identity).
 constexpr int ID_ITERS = WB / (WAVES * 4);          // rows per thread in the pointwise pass (16)
-#ifndef RDN_CBAM_RELOAD_A
-#define RDN_CBAM_RELOAD_A 0
-#endif
 // identity rows fetched ahead of the spatial pass (the rest at the write-back): all 16 for fp32 and
 // f16f8 (3 VGPRs per row there), 8 for split-bf16 (16 spill there; measured 18.8k vs 16.5k APIDN
 // spectra/s); plain bf16 keeps its identity in LDS
-#ifdef RDN_CBAM_ID_PRE
-template <int MODE> constexpr int ID_PRE = RDN_CBAM_ID_PRE;
-#else
 template <int MODE> constexpr int ID_PRE = MODE == MODE_X3 ? 8 : 16;
-#endif
 
 template <int MODE>
 __device__ __forceinline__ void apply_cbam(Tile& tl, const TeamArgs& ta, const char* slots0, int cbam_slot, bool bias, int res,
@@ -770,8 +763,7 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
   char* tslots = ta.slots + (size_t)team * 2 * ta.TT * SLOT_BYTES;
   constexpr int NL = ADS ? 32 : 30;             // big layers
   // the next layer's weights: prefetched by the conv before a CBAM (held across it), or loaded
-  // after it (RDN_CBAM_RELOAD_A: frees their VGPRs during the CBAM)
-  constexpr bool RELOAD_A = RDN_CBAM_RELOAD_A;
+  constexpr bool RELOAD_A = false;
   unsigned nbar = 0;
   f32x4 id[16];
   Stamps stamp;
@@ -879,7 +871,7 @@ using V = h16c::V;
 constexpr int WB16 = h16c::WB;
 constexpr int NT = h16c::NT;
 constexpr int EDGE16_BYTES = EDGE_ROWS * h16c::ROWB;        // one edge, f16 rows
-// RDN_T16_TAGGED (default): the hand-off carries its own completion -- every 4-byte word of a slot
+// The hand-off carries its own completion -- every 4-byte word of a slot
 // travels as an 8-byte granule {word, tag} written by one sc1 store (tag = the CBAM's sequence
 // number + 1; the slots are zeroed before each launch), and a consumer polls the granules it needs
 // until every tag is current.  The producer neither drains its stores nor meets a counter, and the
@@ -887,46 +879,17 @@ constexpr int EDGE16_BYTES = EDGE_ROWS * h16c::ROWB;        // one edge, f16 row
 // of drain + counter add + counter poll + slot loads: MI355X_MICROARCH.md handoff-1to1 vs
 // handoff-flag).  Slot = 64 channel sums (f32: each tile's sum of its fp32 lane partials, rounded
 // once) | 64 ordered maxima | 2 x EDGE_ROWS rows of u (f16) as 4-byte words.
-#ifndef RDN_T16_TAGGED
-#define RDN_T16_TAGGED 1
-#endif
 constexpr int G_SUM = 0, G_MAX = 64, G_EDGE = 128;               // granule indices within a slot
-constexpr bool RDN_T16_TAGGED_ON = RDN_T16_TAGGED;
-// RDN_T16_SA_LOCAL=1: per-wave conv7 with recomputed halo rows instead of a separate pass (one
-// barrier fewer): measured 0.4 % (ADSDN) / 2 % (APIDN) SLOWER with the tagged hand-off (the extra
-// 16-lane group and the wave-serial conv7 cost more than the barrier), so off
-#ifndef RDN_T16_SA_LOCAL
-#define RDN_T16_SA_LOCAL 0
-#endif
-// RDN_T16_MEAN_MFMA=1: the spatial mean over channels as two MFMAs per row group (A = ca); 0: packed
-// f16 adds and a cross-lane sum
-#ifndef RDN_T16_MEAN_MFMA
-#define RDN_T16_MEAN_MFMA 1
-#endif
-// RDN_T16_SA_PAIR=1: the spatial conv7 two rows per thread, one round
-#ifndef RDN_T16_SA_PAIR
-#define RDN_T16_SA_PAIR 1
-#endif
-// RDN_T16_MLP_BFLY=1: the channel-attention MLP's 8 hidden sums by one lane butterfly
-#ifndef RDN_T16_MLP_BFLY
-#define RDN_T16_MLP_BFLY 1
-#endif
-#ifndef RDN_T16_POLL_PER
-#define RDN_T16_POLL_PER 4
-#endif
-// RDN_T16_XCD=1: teams placed on one XCD each (see team16_forward) hand off through that XCD's L2
-// (plain slot stores) once the launch's first CBAM has confirmed the placement
-#ifndef RDN_T16_XCD
-#define RDN_T16_XCD 1
-#endif
+// The spatial mean over channels runs as two MFMAs per row group (A = ca), the spatial conv7 two
+// rows per thread in one round, the channel-attention MLP's 8 hidden sums as one lane butterfly
+// (DESIGN.md §3 CBAM table; a per-wave conv7 with recomputed halo rows measured 0.4-2 % slower).
+// Teams placed on one XCD each (team16_forward) hand off through that XCD's L2 (plain slot stores)
+// once the launch's first CBAM has confirmed the placement.
+constexpr int POLL_PER = 4;                                      // poll rounds batched per wave
 // s_getreg operand of HW_REG_XCC_ID (id 20), bits [3:0]
 constexpr int HWREG_XCC_ID = (3 << 11) | 20;
 constexpr int EDGE16_WORDS = EDGE16_BYTES / 4;                   // 160 per edge
-#if RDN_T16_TAGGED
 constexpr int SLOT16_BYTES = (G_EDGE + 2 * EDGE16_WORDS) * 8;    // 448 granules = 3584 B
-#else
-constexpr int SLOT16_BYTES = STAT_BYTES + 2 * EDGE16_BYTES;
-#endif
 // CBAM scratch in BUF1
 constexpr int SC = h16c::BUF1;
 constexpr int RED16_OFF = SC;                                  // [4 row blocks][64] f32 sums, then u32 maxima
@@ -1004,7 +967,7 @@ template <int AUX>
 __device__ __forceinline__ void slot_store128(u32x4 v, __amdgpu_buffer_rsrc_t sr, int off) {
   __builtin_amdgcn_raw_buffer_store_b128(v, sr, off, 0, AUX);
 }
-// xmode (RDN_T16_XCD): XM_PROBE = the launch's first CBAM (sc1 stores; every sum granule's tag carries
+// xmode: XM_PROBE = the launch's first CBAM (sc1 stores; every sum granule's tag carries
 // bit 31 when this tile cannot hand off through its XCD's L2), XM_L2 = plain stores (the line stays
 // in the team's one L2, which every member's L1-bypassing loads read), XM_SC1 = sc1 stores
 enum XMode : int { XM_PROBE = 0, XM_L2 = 1, XM_SC1 = 2 };
@@ -1054,7 +1017,6 @@ __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& 
     }
   }
   __syncthreads();
-#if RDN_T16_TAGGED
   // one store phase, no drain, no arrival: the statistics (wave 0: granules {f32 sum, tag} and
   // {ordered max, tag}) and the edge rows (u, f16) for the neighbours (waves 1-2: two granules per
   // 16-B sc1 store): block 0 = rows [2H - 5, 2H) (the left neighbour's rows [WB - 5, WB)), block 1 =
@@ -1092,35 +1054,6 @@ __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& 
     }
   }
   (void)ctr;
-#else
-  // one store phase: the statistics (wave 0) and the edge rows (u, f16) for the neighbours (waves
-  // 1-2): block 0 = rows [2H - 5, 2H) (the left neighbour's rows [WB - 5, WB)), block 1 = rows
-  // [T, T + 5); every storing wave drains its stores, the workgroup barrier, then the arrival
-  if (tid < 64) {
-    const int c = tid;
-    double sv = 0.0;
-    unsigned m = 0;
-#pragma unroll
-    for (int k = 0; k < h16c::RB; ++k) {
-      sv += (double)rs[k * 64 + c];
-      m = max(m, rm[k * 64 + c]);
-    }
-    __hip_atomic_store((double*)slot + c, sv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((unsigned*)(slot + 512) + c, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if (tid < 64 + 2 * EDGE_ROWS * 8) {
-    const int i = tid - 64, e = i / (EDGE_ROWS * 8), k = (i / 8) % EDGE_ROWS, g = i & 7;
-    const int r = e == 0 ? WB16 - T - EDGE_ROWS + k : T + k;
-    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slot, 0, SLOT16_BYTES, 0x00020000);
-    const u32x4 v = *(const u32x4*)(lds + h16c::BUF0 + h16c::soff(r, g));
-    __builtin_amdgcn_raw_buffer_store_b128(v, sr, STAT_BYTES + e * EDGE16_BYTES + (k * 8 + g) * 16, 0, 16);
-  }
-  if (tid < 64 + 2 * EDGE_ROWS * 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0 && arrive) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  (void)tag;
-  (void)xmode;
-  (void)local;
-#endif
 }
 
 // apply the CBAM whose statistics sit in the team's slots to u (BUF0): h = [identity +] u*ca*sa
@@ -1142,7 +1075,6 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   const float b2 = bias ? cmisc[4 + lane] : 0.f;
   const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void*)slots0, 0, ta.TT * SLOT16_BYTES, 0x00020000);
 
-#if RDN_T16_TAGGED
   // the granules this thread needs, polled until every tag is `tag` (uniform loop: one workgroup
   // vote per round): the halo refresh (threads < 80: u of rows [0, 5) from the left neighbour's
   // block 1, rows [WB - 5, WB) from the right neighbour's block 0; first / last tile: no
@@ -1163,7 +1095,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
     const int c = tid & 63, part = tid >> 6;
     // slots per thread per poll batch: 4 -> one batch (one round trip) for up to 32 tiles, i.e. up to
     // L = 20,096 (L = 16,384: 27 tiles; 2 per thread made that two batches polled one after the other)
-    constexpr int PER = RDN_T16_POLL_PER, STEP = h16c::WAVES * PER;
+    constexpr int PER = POLL_PER, STEP = h16c::WAVES * PER;
     const int nbatch = (ta.TT + STEP - 1) / STEP;
     // this tile's own slot is not polled: its granules are the values publish16 stored, recomputed
     // from the same LDS partials in the same order (same bits), so the last tile to publish goes on
@@ -1257,58 +1189,6 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
     *(u32x4*)(lds + h16c::BUF0 + h16c::soff(r, edge_g)) = u32x4{ea[0], ea[2], eb[0], eb[2]};
   }
   __syncthreads();
-#else
-  // halo refresh, fetched first: u of rows [0, 5) from the left neighbour's block 1, rows
-  // [WB - 5, WB) from the right neighbour's block 0 (first / last tile: no neighbour)
-  const int edge_e = tid / (EDGE_ROWS * 8), edge_k = (tid / 8) % EDGE_ROWS, edge_g = tid & 7;
-  bool has_edge = false;
-  u32x4 edge_u = {0u, 0u, 0u, 0u};
-  if (tid < 2 * EDGE_ROWS * 8) {
-    const int tile = (tl.base + ta.halo) / ta.T;
-    const int nb = edge_e == 0 ? tile - 1 : tile + 1;
-    if (nb >= 0 && nb < ta.TT) {
-      edge_u = __builtin_amdgcn_raw_buffer_load_b128(
-          sr, nb * SLOT16_BYTES + STAT_BYTES + (1 - edge_e) * EDGE16_BYTES + (edge_k * 8 + edge_g) * 16, 0, 16);
-      has_edge = true;
-    }
-  }
-  // the spectrum's per-channel mean and max over the TT slots, combined in a fixed order
-  double* pool = (double*)(lds + POOL_OFF);
-  {
-    const int c = tid & 63, part = tid >> 6;
-    double sp = 0.0;
-    unsigned mp = 0;
-    constexpr int PER = 2;                 // 16 slots per batch (TT = 16 at L = 10,000)
-    for (int t0 = part; t0 < ta.TT; t0 += h16c::WAVES * PER) {
-      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-      u32x2 sv[PER];
-      unsigned mv[PER];
-#pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const int t = t0 + h16c::WAVES * k;
-        const int off = (t < ta.TT ? t : 0) * SLOT16_BYTES;
-        sv[k] = __builtin_amdgcn_raw_buffer_load_b64(sr, off + 8 * c, 0, 16);
-        mv[k] = __builtin_amdgcn_raw_buffer_load_b32(sr, off + 512 + 4 * c, 0, 16);
-      }
-#pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        if (t0 + h16c::WAVES * k < ta.TT) {
-          sp += __builtin_bit_cast(double, sv[k]);
-          mp = max(mp, mv[k]);
-        }
-      }
-    }
-    double* ps = (double*)(lds + SLP_OFF);
-    unsigned* pm = (unsigned*)(lds + SLP_OFF + 8 * 64 * 8);
-    ps[part * 64 + c] = sp;
-    pm[part * 64 + c] = mp;
-  }
-  if (has_edge) {
-    const int r = edge_e == 0 ? edge_k : WB16 - EDGE_ROWS + edge_k;
-    *(u32x4*)(lds + h16c::BUF0 + h16c::soff(r, edge_g)) = edge_u;
-  }
-  __syncthreads();
-#endif
   st(10);
   // channel attention, evaluated whole by every wave (no barrier): the pooled avg / max of channel
   // `lane` from the 8 partials in a fixed order, the 4 + 4 hidden units as sums over the 64 lanes
@@ -1324,7 +1204,6 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
       m = max(m, pm[k * 64 + lane]);
     }
     const float pa = (float)sum * __builtin_amdgcn_rcpf((float)tl.L), px = ord2f(m);
-#if RDN_T16_MLP_BFLY
     // the 8 hidden sums (fc.0 row j of the pooled avg / max, over the 64 lanes = channels) by one
     // butterfly instead of 8 separate reductions: lane halves swap (avg | max), then lane quarters
     // (j pairs), rows of 8 (ror 8), and 3 DPP adds finish each 8-lane group; lane 8g of the wave then
@@ -1356,18 +1235,6 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
       oa = fmaf(cw2v[j], ha + hm, oa);
     }
     cav = sigm_fast(oa);
-#else
-    float oa = b2, om = b2;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float b1 = bias ? cmisc[j] : 0.f;
-      const float ha = fmaxf(quarter_sum(row_sum(w1v[j] * pa)) + b1, 0.f);
-      const float hm = fmaxf(quarter_sum(row_sum(w1v[j] * px)) + b1, 0.f);
-      oa = fmaf(cw2v[j], ha, oa);
-      om = fmaf(cw2v[j], hm, om);
-    }
-    cav = sigm_fast(oa + om);
-#endif
   }
   // this lane's 8 channels of ca through the wave's own LDS row (in-order within a wave)
   float* caw = (float*)(lds + CA16_OFF) + 64 * w;
@@ -1392,63 +1259,6 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   float* m2 = (float*)(lds + M2_OFF) + 3;      // the tile and [0, L)
   constexpr int SROWS = WB16 / h16c::WAVES;    // 80 rows per wave
   static_assert(SROWS % 16 == 0, "whole 16-row groups per wave");
-#if RDN_T16_SA_LOCAL
-  // RDN_T16_SA_LOCAL: each wave also forms [mean; max] of the 3 + 3 rows around its own
-  // 80 (one extra 16-lane group, lanes c16 < 6; rows outside the tile are 0) and then runs the conv7
-  // of its own rows from its own LDS writes (in order within a wave): no workgroup barrier and no
-  // separate pass between the spatial statistics and sa.  A halo row is written by two waves with
-  // the same value.
-  float* sa = (float*)(lds + SA16_OFF);
-  {
-    constexpr int KG = SROWS / 16;
-    auto srow = [&](int k) {                   // row of group k for this lane (k == KG: the halo group)
-      return k < KG ? SROWS * w + ln.c16 + 16 * k
-                    : (ln.c16 < 3 ? SROWS * w - 3 + ln.c16 : SROWS * w + SROWS + min(ln.c16, 5) - 3);
-    };
-    V ua[KG + 1], ub[KG + 1];
-#pragma unroll
-    for (int k = 0; k <= KG; ++k) {
-      const int r = min(max(srow(k), 0), WB16 - 1);
-      ua[k] = *(const V*)(lds + h16c::BUF0 + h16c::soff(r, ln.q));
-      ub[k] = *(const V*)(lds + h16c::BUF0 + h16c::soff(r, ln.q + 4));
-    }
-#pragma unroll
-    for (int k = 0; k <= KG; ++k) {
-      const V va = ua[k] * cq0, vb = ub[k] * cq4;
-      const V vs = va + vb, vm = __builtin_elementwise_max(va, vb);
-      const h2 s2 = (__builtin_shufflevector(vs, vs, 0, 1) + __builtin_shufflevector(vs, vs, 2, 3)) +
-                    (__builtin_shufflevector(vs, vs, 4, 5) + __builtin_shufflevector(vs, vs, 6, 7));
-      const h2 x2 = __builtin_elementwise_max(
-          __builtin_elementwise_max(__builtin_shufflevector(vm, vm, 0, 1), __builtin_shufflevector(vm, vm, 2, 3)),
-          __builtin_elementwise_max(__builtin_shufflevector(vm, vm, 4, 5), __builtin_shufflevector(vm, vm, 6, 7)));
-      const float sm = quarter_sum((float)s2[0] + (float)s2[1]);
-      const float mx = quarter_max(fmaxf((float)x2[0], (float)x2[1]));
-      if (ln.q == 0 && (k < KG || ln.c16 < 6)) {
-        const int r = srow(k);
-        const bool in = r >= 0 && r < WB16 && h16c::in_range(tl.base + r, tl.L);
-        m1[r] = in ? sm * (1.0f / 64.0f) : 0.f;
-        m2[r] = in ? mx : 0.f;
-      }
-    }
-    // sa = sigmoid(conv7([mean_c; max_c])) of this wave's rows
-#pragma unroll
-    for (int i = 0; i < (SROWS + 63) / 64; ++i) {
-      const int j = lane + 64 * i;
-      if (j < SROWS) {
-        const int r = SROWS * w + j;
-        float a = bias ? cmisc[82] : 0.f;
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {
-          a = fmaf(cmisc[68 + k], m1[r + k - 3], a);
-          a = fmaf(cmisc[75 + k], m2[r + k - 3], a);
-        }
-        sa[r] = sigm_fast(a);
-      }
-    }
-  }
-  __syncthreads();
-  st(12);
-#else
   {
     V ua[SROWS / 16], ub[SROWS / 16];
 #pragma unroll
@@ -1461,19 +1271,12 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
     for (int k = 0; k < SROWS / 16; ++k) {
       const V va = ua[k] * cq0, vb = ub[k] * cq4;
       const V vm = __builtin_elementwise_max(va, vb);
-#if RDN_T16_MEAN_MFMA
       // sum_c ca_c u_c of row c16 on the idle MFMA pipe: A = ca (every row of the 16 x 32 A-operand
       // the same, its K order the B-fragment channel order of slots q / q + 4: cq0 / cq4), B = the
       // two u fragments this lane holds anyway; every output row is the sum, exact f16 products
       // accumulated in fp32 -- no pk_add tree and no cross-lane sum
       const f32x4 dsum = h16c::mma(cq4, ub[k], h16c::mma(cq0, ua[k], (f32x4)(0.f)));
       const float sm = dsum[0];
-#else
-      const V vs = va + vb;
-      const h2 s2 = (__builtin_shufflevector(vs, vs, 0, 1) + __builtin_shufflevector(vs, vs, 2, 3)) +
-                    (__builtin_shufflevector(vs, vs, 4, 5) + __builtin_shufflevector(vs, vs, 6, 7));
-      const float sm = quarter_sum((float)s2[0] + (float)s2[1]);
-#endif
       const h2 x2 = __builtin_elementwise_max(
           __builtin_elementwise_max(__builtin_shufflevector(vm, vm, 0, 1), __builtin_shufflevector(vm, vm, 2, 3)),
           __builtin_elementwise_max(__builtin_shufflevector(vm, vm, 4, 5), __builtin_shufflevector(vm, vm, 6, 7)));
@@ -1495,7 +1298,6 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   st(12);
   // sa = sigmoid(conv7([mean_c; max_c]))
   float* sa = (float*)(lds + SA16_OFF);
-#if RDN_T16_SA_PAIR
   // two adjacent rows per thread (their 7-tap windows share 6 rows): the 320 row pairs of the tile
   // in one round instead of 640 rows in two
   for (int i = tid; i < WB16 / 2; i += h16c::THREADS) {
@@ -1517,20 +1319,8 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
     sa[r] = sigm_fast(a0);
     sa[r + 1] = sigm_fast(a1);
   }
-#else
-  for (int r = tid; r < WB16; r += h16c::THREADS) {
-    float a = bias ? cmisc[82] : 0.f;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      a = fmaf(cmisc[68 + k], m1[r + k - 3], a);
-      a = fmaf(cmisc[75 + k], m2[r + k - 3], a);
-    }
-    sa[r] = sigm_fast(a);
-  }
-#endif
   __syncthreads();
   st(13);
-#endif
   V uv[NT];
   // h = [identity +] u*ca*sa [relu], in place, packed f16; rows outside [0, L) zero
   float sv[NT];
@@ -1559,7 +1349,7 @@ __device__ __forceinline__ void team16_spectra(char* lds, const uint8_t* blob, c
                                                float* y, int L, const TeamArgs& ta, int team, int tile,
                                                bool local) {
   unsigned* ctr = ta.counters + (size_t)team * TEAM_CTR_STRIDE;
-  int xmode = RDN_T16_TAGGED && RDN_T16_XCD && ta.xcd ? XM_PROBE : XM_SC1;
+  int xmode = ta.xcd ? XM_PROBE : XM_SC1;
   char* tslots = ta.slots + (size_t)team * 2 * ta.TT * SLOT16_BYTES;
   unsigned nbar = 0;
   Stamps st;
@@ -1582,9 +1372,6 @@ __device__ __forceinline__ void team16_spectra(char* lds, const uint8_t* blob, c
       st(1);
       publish16(tl, ta, mine, ctr, !skip, pre, ta.tag0 + nbar + 1, xmode, local);
       st(3);
-#if !RDN_T16_TAGGED
-      team_wait(ta, ctr, (nbar + 1) * (unsigned)ta.TT);
-#endif
       st(4);
       apply16<EDGE>(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT16_BYTES, slot, ADS, res, id, st,
                     ta.tag0 + nbar + 1, xmode, local);
@@ -1643,7 +1430,6 @@ __global__ __launch_bounds__(h16c::THREADS) void team16_forward(const uint8_t* _
   const int wg = __builtin_amdgcn_workgroup_id_x();
   int team = wg / ta.TT, tile = wg - team * ta.TT;
   bool local = false;
-#if RDN_T16_XCD
   // XCD-aware teams: workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md), so
   // workgroups 8r + x, r < R0, sit on XCD x; they form teams 8j + x of TT tiles (r = j TT + tile),
   // each on one XCD, and the workgroups from 8 R0 on form the remaining teams in order.  A member
@@ -1658,7 +1444,6 @@ __global__ __launch_bounds__(h16c::THREADS) void team16_forward(const uint8_t* _
     team = 8 * tpx + (wg - 8 * R0) / ta.TT;
     tile = (wg - 8 * R0) % ta.TT;
   }
-#endif
   const int base = tile * ta.T - ta.halo;
   // a tile holds positions outside [0, L) for every spectrum or for none (one L per launch)
 #if defined(RDN_ABLATE_ALLEDGE)          // diagnostic: every tile on the edge-tile code
@@ -1742,9 +1527,8 @@ static TeamGeo team_geo(int arch, int mode, int64_t L, int dev) {
   // the ping-pong team kernel spreads L evenly over its TT tiles (T = ceil(L / TT) own positions;
   // the rows beyond them up to the tile's end are its right halo): the last tile then holds few
   // rows outside [0, L) (9 instead of 54 at L = 10,000), whose zeroing after every conv made it
-  // the slowest member of its team.  RDN_T16_FULL_T=1: every tile owns WB - 2 halo (A/B knob).
-  const char* full = getenv("RDN_T16_FULL_T");
-  if (p16 && !(full && full[0] == '1')) g.T = (int)((L + g.TT - 1) / g.TT);
+  // the slowest member of its team (+0.5-0.7 % against tiles that each own WB - 2 halo).
+  if (p16) g.T = (int)((L + g.TT - 1) / g.TT);
   const int resident = device_cus(dev) * team_blocks_per_cu(arch, mode, dev);
   g.teams = resident > 0 ? resident / g.TT : 0;
   const char* env = getenv("RDN_CBAM_SEGMENTS");       // diagnostics: force the per-segment path
@@ -1798,11 +1582,11 @@ static hipError_t launch_team(int arch, int mode, const TeamGeo& g, const uint8_
   // the sticky word after it collects every launch's timeouts until cbam_status reads and clears it
   hipError_t e = hipMemsetAsync(ta.counters, 0, g.counters, stream);
   if (e == hipSuccess) e = hipMemsetAsync(ta.err, 0, 4, stream);
-  // the tagged hand-off (RDN_T16_TAGGED) starts from tag 0 in every slot granule, and each launch
+  // the tagged hand-off starts from tag 0 in every slot granule, and each launch
   // takes tags from a range no earlier launch used (ta.tag0, below): no granule of an earlier launch
-  // -- in memory or left in an XCD's L2 by plain stores (RDN_T16_XCD) -- carries a tag this launch
+  // -- in memory or left in an XCD's L2 by plain stores -- carries a tag this launch
   // waits for
-  if (e == hipSuccess && mode == MODE_P16 && cb::t16::RDN_T16_TAGGED_ON) e = hipMemsetAsync(ta.slots, 0, g.slots, stream);
+  if (e == hipSuccess && mode == MODE_P16) e = hipMemsetAsync(ta.slots, 0, g.slots, stream);
   if (e != hipSuccess) return e;
   const int64_t teams = n < g.teams ? n : g.teams;    // never more teams than spectra
   ta.teams = (int)teams;

@@ -78,58 +78,36 @@ constexpr int BIAS_OFF = H16_BIAS_OFF;
 #ifndef RDN_H16_PF
 #define RDN_H16_PF 3
 #endif
-#ifndef RDN_H16_PKRELU
-#define RDN_H16_PKRELU 1
-#endif
-// RDN_H16_M32: the layer as v_mfma_f32_32x32x16 (32 output channels x 32 positions x 16 K per
-// MFMA: half the MFMA instructions of the 16x16x32 form for the same work, so each one leaves 24 of
-// its 32 cycles of vector issue to the LDS reads, weight loads and epilogue instead of 8 of 16).
-#ifndef RDN_H16_M32
-#define RDN_H16_M32 0
-#endif
-// RDN_H16_EDGE_POST: a tile holding positions outside [0, L) stores its layer outputs unmasked (the
-// MFMA loop is the interior tiles' own) and each wave then zeroes its rows outside [0, L) -- a few
-// stores after the loop, before the barrier; 0 = a per-lane range check and select in every epilogue
-// (the edge tiles of a spectrum then ran ~10 % slower: the CBAM team kernel waits for them)
-#ifndef RDN_H16_EDGE_POST
-#define RDN_H16_EDGE_POST 1
-#endif
+// A tile holding positions outside [0, L) stores its layer outputs unmasked (the MFMA loop is the
+// interior tiles' own) and each wave then zeroes its rows outside [0, L) -- a few stores after the
+// loop, before the barrier (zero_outside; a per-lane range check and select in every epilogue made
+// the edge tiles ~10 % slower, and the CBAM team kernel waits for them).  The 32x32x16 MFMA form
+// measured 5 % slower (same MFMA busy, lower clock) and is not built.
 constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
 constexpr int MH = 2;                                 // output-channel halves (32 channels each)
 constexpr int RB = WAVES / MH;                        // row blocks
 constexpr int RW = WB / RB;                           // 160 rows per wave
-#if RDN_H16_M32
-constexpr int NR = 32;                                // positions per N-tile
-constexpr int KS = 12;                                // k-steps per layer (3 taps x 4 x 16 channels)
-constexpr int NFRAG = 12;                             // A-fragments per wave per layer
-constexpr int NBIAS = 4;                              // 16-B bias loads per wave per layer
-constexpr int HEAD_LANES = 32;
-#else
 constexpr int NR = 16;
 constexpr int KS = 6;                                 // 3 taps x 2 x 32 channels
 constexpr int NFRAG = 12;                             // 2 M-tiles x 6 k-steps
 constexpr int NBIAS = 2;
 constexpr int HEAD_LANES = 16;
-#endif
 constexpr int NT = RW / NR;                           // N-tiles per wave (10 / 5)
 constexpr int HN = (NT + MH - 1) / MH;                // head N-tiles per wave (the two halves split the rows)
 static_assert(RW % NR == 0, "rows per wave must be whole N-tiles");
 static_assert((WB % 64) == 0 && (THREADS % 64) == 0, "stem items must not straddle a slot within a wave");
 
 typedef float f32x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 #if RDN_H16_F16
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 typedef f16x8_t V;
 typedef _Float16 E;
 __device__ __forceinline__ f32x4 mma(V a, V b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
-__device__ __forceinline__ f32x16 mma(V a, V b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
 #else
 typedef bf16x8 V;
 typedef __bf16 E;
 __device__ __forceinline__ f32x4 mma(V a, V b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
-__device__ __forceinline__ f32x16 mma(V a, V b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0); }
 #endif
 // Thread index the compiler cannot treat as loop-invariant (per-lane addresses are recomputed where
 // they are used instead of being hoisted across the network's layers and spilled)
@@ -138,18 +116,7 @@ __device__ __forceinline__ int tid() {
   asm volatile("" : "+v"(t));
   return t;
 }
-#if RDN_H16_M32
-// 32x32x16 B reads: a ds_read_b128 lane group holds 16 rows that are distinct mod 16, all at one
-// slot, so (row & 1, slot ^ f(row)) must be distinct over row mod 16 (a 128-B row spans half the
-// 64 banks); the 16-B epilogue stores (8 consecutive aligned rows per lane group, one slot) need f
-// distinct over 8 aligned rows.  f = (row & 7) ^ ((row >> 3) & 1) does both; 640 = 0 mod 16, so a
-// wrapped tap keeps the swizzle.
-__device__ __forceinline__ int soff(int row, int slot) {
-  return row * ROWB + ((slot ^ (row & 7) ^ ((row >> 3) & 1)) << 4);
-}
-#else
 __device__ __forceinline__ int soff(int row, int slot) { return row * ROWB + ((slot ^ (row & 7)) << 4); }
-#endif
 __device__ __forceinline__ int wrap(int row) { return row < 0 ? row + WB : (row >= WB ? row - WB : row); }
 __device__ __forceinline__ bool in_range(int p, int L) { return (unsigned)p < (unsigned)L; }
 // LDS-only workgroup barrier: this wave's LDS traffic drains, its global loads (next layer's
@@ -167,14 +134,13 @@ struct Tile {
   int layer;             // big layer whose fragments are in VGPRs
   // per-lane LDS offsets, computed once per tile (no address arithmetic at each layer's start):
   // koff[d + 2][u] = soff(r0 + d, 4u + q) for tap shift d in -2..2 (no wrap), r0 = this lane's
-  // first row ((w % RB) * RW + lane % 16); M32: koff[d + 2][v] = soff(r0 + d, 2v + lane / 32),
-  // r0 = (w % RB) * RW + lane % 32
+  // first row ((w % RB) * RW + lane % 16)
   int koff[5][KS / 3];
   int r0;
 };
 
 struct Frags {            // one layer's operands in VGPRs: this wave's A-fragments and folded bias
-  V a[NFRAG];             // 16x16x32: [M-tile 2][k-step 6]; 32x32x16: [k-step 12]
+  V a[NFRAG];             // [M-tile 2][k-step 6]
   f32x4 bias[NBIAS];
 };
 // this wave's output-channel half (channels 32h .. 32h + 31), wave-uniform
@@ -187,54 +153,20 @@ struct LaneOff {          // this lane's byte offsets of the A-fragment and bias
   int a, b;
 };
 // One opaque tid() per layer, not one per load.  The blob's fragments are 16x16x32 A-operands,
-// fragment (m, s = 2t + u) lane r + 16q = W[16m + r][slot 4u + q of tap t] (pack.cpp).  M32 gathers
-// its 32x32x16 A-operand for k-step (t, v) from them: lane r + 32e needs cout 32h + r at slot
-// g = 2v + e, i.e. fragment (2h + r / 16, 2t + v / 2), lane (r % 16) + 16 (2 (v % 2) + e) -- a
-// per-lane part (below) plus a wave-uniform one (load_op); bias regs 4j..4j+3 of lane 32e + r are
-// couts 32h + 8j + 4e + 0..3.
+// fragment (m, s = 2t + u) lane r + 16q = W[16m + r][slot 4u + q of tap t] (pack.cpp).
 __device__ __forceinline__ LaneOff lane_off() {
   const int lane = tid() & 63;
-#if RDN_H16_M32
-  return {((lane >> 4) & 1) * 6 * 1024 + (lane & 15) * 16 + (lane >> 5) * 256, (lane >> 5) * 16};
-#else
   return {lane * 16, (lane >> 4) * 16};
-#endif
 }
-// RDN_H16_LDORDER 1: the next layer's operands are fetched in the order its first N-tile consumes
-// them (the bias vectors, the C operand of its first MFMAs, first; then the fragments k-step by
-// k-step), so the waits at a layer's start cover only the oldest loads
-#ifndef RDN_H16_LDORDER
-#define RDN_H16_LDORDER 0
-#endif
 // operand i of half h of big layer `layer`: A-fragment i (< NFRAG) or bias vector i - NFRAG
 __device__ __forceinline__ void load_op(const Tile& tl, int layer, int h, int i, const LaneOff& lo, Frags& F) {
-#if RDN_H16_LDORDER && !RDN_H16_M32
-  i = i < NBIAS ? NFRAG + i : (i - NBIAS) % 2 * 6 + (i - NBIAS) / 2;
-#elif RDN_H16_LDORDER
-  i = i < NBIAS ? NFRAG + i : i - NBIAS;
-#endif
   const int base = layer * LAYER_BYTES;
-#if defined(RDN_ABLATE_WSAME)             // diagnostic (wrong results): both halves fetch half 0's operands
-  h = 0;
-#endif
-#if defined(RDN_ABLATE_WHALF)             // diagnostic (wrong results): half the fragment loads
-  if (i < NFRAG && (i & 1)) return;
-#endif
   if (i < NFRAG) {
-#if RDN_H16_M32
-    const int t = i >> 2, v = i & 3;
-    const int so = base + (12 * h + 2 * t + (v >> 1)) * 1024 + (v & 1) * 512;
-#else
     const int so = base + ((2 * h + i / 6) * 6 + i % 6) * 1024;
-#endif
     F.a[i] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, lo.a, so, 0));
   } else {
     const int j = i - NFRAG;
-#if RDN_H16_M32
-    const int so = base + BIAS_OFF + 128 * h + 32 * j;
-#else
     const int so = base + BIAS_OFF + 64 * (2 * h + j);
-#endif
     F.bias[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, lo.b, so, 0));
   }
 }
@@ -247,27 +179,12 @@ __device__ __forceinline__ void load_frags(const Tile& tl, int layer, Frags& F) 
   for (int i = 0; i < NLOAD; ++i) load_op(tl, layer, h, i, lo, F);
 }
 
-// Accumulators of one N-tile: 16x16x32: M-tiles 2h, 2h + 1 (16 channels x 16 positions each);
-// 32x32x16: one 32 x 32 tile.  Start at the folded bias.
+// Accumulators of one N-tile: M-tiles 2h, 2h + 1 (16 channels x 16 positions each), started at the
+// folded bias.
 struct Acc {
-#if RDN_H16_M32
-  f32x16 v;
-#else
   f32x4 v[2];
-#endif
 };
 __device__ __forceinline__ void mstep(const Frags& F, int s, V b, Acc& acc) {
-#if RDN_H16_M32
-  const f32x16 bias = __builtin_shufflevector(__builtin_shufflevector(F.bias[0], F.bias[1], 0, 1, 2, 3, 4, 5, 6, 7),
-                                              __builtin_shufflevector(F.bias[2], F.bias[3], 0, 1, 2, 3, 4, 5, 6, 7),
-                                              0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
-#if defined(RDN_ABLATE_NOMFMA)
-  if (s == 0) acc.v = bias;
-  asm volatile("" : "+v"(acc.v) : "v"(F.a[s]), "v"(b));
-#else
-  acc.v = mma(F.a[s], b, s == 0 ? bias : acc.v);
-#endif
-#else
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
 #if defined(RDN_ABLATE_NOMFMA)
@@ -277,22 +194,18 @@ __device__ __forceinline__ void mstep(const Frags& F, int s, V b, Acc& acc) {
     acc.v[m] = mma(F.a[m * 6 + s], b, s == 0 ? F.bias[m] : acc.v[m]);
 #endif
   }
-#endif
 }
 
 // Conv1d(1, 64, 3, padding=1) (+ folded BN) + ReLU in fp32, one (row, 16-B slot) item per lane
 // and step.  ACCUM adds the result onto the resident row (PIDN/train.py:105, identity recomputed
 // from x).  out_lo / out_hi (lo <= hi): returns whether any input this thread read at the tile's
 // rows lies outside [lo, hi] (the RDN_F16MIX spiked-tile test, rrcdnet_hybrid.hpp), else false.
-// RDN_H16_STEM2 (default): wave w computes slot w (8 channels, its 32 weights scalar-loaded once)
-// for rows lane + 64k, and every x value of those rows is fetched before the first is used (buffer
-// loads: positions outside [0, L) read 0 by the range check of the resource) -- one memory latency
-// per stem instead of one per item (the item loop kept the stem on its loads: 7 % of the RDN_F16MIX
-// hybrid, which runs two stems per tile).  Same arithmetic per value as the item loop (bit-equal).
-// RDN_H16_STEM2=2: channel pairs on v_pk_fma_f32 and a packed ReLU after the rounding (no ACCUM)
-#ifndef RDN_H16_STEM2
-#define RDN_H16_STEM2 2
-#endif
+// Wave w computes slot w (8 channels, its 32 weights scalar-loaded once) for rows lane + 64k, and
+// every x value of those rows is fetched before the first is used (buffer loads: positions outside
+// [0, L) read 0 by the range check of the resource) -- one memory latency per stem (a loop of one
+// (row, slot) item per lane and step waited on its loads ten times: 7 % of the RDN_F16MIX hybrid,
+// which runs two stems per tile); channel pairs on v_pk_fma_f32 and a packed ReLU after the rounding
+// (without ACCUM).
 template <bool ACCUM = false>
 __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, float out_lo = 1.f, float out_hi = 0.f) {
   const float* swp = tl.small + sslot * SMALL_SLOT_FLOATS;
@@ -302,7 +215,6 @@ __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, fl
 #if defined(RDN_ABLATE_NOSTEM)         // diagnostic (tools/ablate.py): the stem's cost, wrong results
   return outside;
 #endif
-#if RDN_H16_STEM2
   static_assert(WB % 64 == 0 && WAVES == 8, "one slot per wave, rows lane + 64k");
   constexpr int NK = WB / 64;
   const int g = __builtin_amdgcn_readfirstlane(tid() >> 6), lane = tid() & 63;
@@ -332,7 +244,6 @@ __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, fl
     if (out_lo <= out_hi) outside = outside || x0[k] < out_lo || x0[k] > out_hi;
     V* ptr = (V*)(tl.lds + dst + soff(row, g));
     V v;
-#if RDN_H16_STEM2 >= 2
     if (!ACCUM) {
       // channel pairs by v_pk_fma_f32 (each half one fmaf, same order), ReLU after the rounding
       // (rounding is monotone and keeps 0: the same value), rows outside [0, L) zeroed last
@@ -352,7 +263,6 @@ __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, fl
       *ptr = v;
       continue;
     }
-#endif
     if (ACCUM) v = *ptr;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -360,33 +270,6 @@ __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, fl
       a = fmaf(wm[j], xm[k], a);
       a = fmaf(w0[j], x0[k], a);
       a = fmaf(wp[j], xp[k], a);
-      a = fmaxf(a, 0.f);
-      if (ACCUM) a += (float)v[j];
-      v[j] = (E)(valid ? a : 0.f);
-    }
-    *ptr = v;
-  }
-  return outside;
-#endif
-  for (int i = tid(); i < WB * 8; i += THREADS) {
-    const int g = __builtin_amdgcn_readfirstlane(i / WB);
-    const int row = i - g * WB;
-    const int p = tl.base + row;
-    const float xm = in_range(p - 1, tl.L) ? tl.x[p - 1] : 0.f;
-    const float x0 = in_range(p, tl.L) ? tl.x[p] : 0.f;
-    const float xp = in_range(p + 1, tl.L) ? tl.x[p + 1] : 0.f;
-    const bool valid = in_range(p, tl.L);
-    if (out_lo <= out_hi) outside = outside || x0 < out_lo || x0 > out_hi;
-    V* ptr = (V*)(tl.lds + dst + soff(row, g));
-    V v;
-    if (ACCUM) v = *ptr;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = h16_channel(g, j);
-      float a = sw[192 + c];
-      a = fmaf(sw[3 * c + 0], xm, a);
-      a = fmaf(sw[3 * c + 1], x0, a);
-      a = fmaf(sw[3 * c + 2], xp, a);
       a = fmaxf(a, 0.f);
       if (ACCUM) a += (float)v[j];
       v[j] = (E)(valid ? a : 0.f);
@@ -475,7 +358,6 @@ template <int EPI, bool EDGE, class SG = NoStage>
 __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int dil, const Frags& F, Frags& G,
                                       bool has_next = true, V* idv = nullptr, ChanStats* cs = nullptr,
                                       SG* stg = nullptr) {
-  static_assert((EPI != LINEAR_SAVE && EPI != STAGE) || !RDN_H16_M32, "LINEAR_SAVE / STAGE: one slot per N-tile");
   const int lane = tid() & 63, w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB;
   const int next = tl.layer + 1;
   asm volatile("" : "+s"(src), "+s"(dst));   // per-layer addresses: not hoisted out of a network's loop (spills)
@@ -502,7 +384,7 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   // bias (+ identity), ReLU, zero rows outside [0, L), round, store 8 channels as one 16-B slot
   auto store_slot = [&](V* p, f32x8 v, bool valid) {
     if (EPI == RES_RELU) v += __builtin_convertvector(*p, f32x8);
-#if RDN_H16_F16 && RDN_H16_PKRELU
+#if RDN_H16_F16
     // ReLU after the rounding, on packed f16 (4 v_pk_max_f16 instead of 8 v_max_f32; the rounding is
     // monotone, so max(f16(v), 0) = f16(max(v, 0)) up to the sign of a zero)
     V hv = __builtin_convertvector(v, V);
@@ -521,22 +403,11 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     *p = __builtin_convertvector(v, V);
 #endif
   };
-#if RDN_H16_M32
-  // lane r + 32e holds channels 32h + (i & 3) + 8 (i >> 2) + 4e of position r in acc reg i: regs
-  // 0-3, 8-11 are slot 4h + e, regs 4-7, 12-15 slot 4h + 2 + e (h16_channel order)
-  const int sa0 = (int)dst + (h ? tl.koff[2][2] : tl.koff[2][0]), sa1 = (int)dst + (h ? tl.koff[2][3] : tl.koff[2][1]);
-  auto epilogue = [&](int n, const Acc& a) {
-    const bool valid = !EDGE || RDN_H16_EDGE_POST || in_range(pos0 + NR * n + (lane & 31), tl.L);
-    store_slot((V*)(tl.lds + sa0 + n * NR * ROWB), __builtin_shufflevector(a.v, a.v, 0, 1, 2, 3, 8, 9, 10, 11), valid);
-    store_slot((V*)(tl.lds + sa1 + n * NR * ROWB), __builtin_shufflevector(a.v, a.v, 4, 5, 6, 7, 12, 13, 14, 15), valid);
-  };
-#else
   const int sa = (int)dst + (h ? tl.koff[2][1] : tl.koff[2][0]);     // slot 4h + q of row r0
   auto epilogue = [&](int n, const Acc& a) {
     // positions outside [0, L): only the N-tiles that straddle 0 or L (a wave-uniform, scalar test)
     // pay the per-lane check and select; the other N-tiles of an edge tile store unmasked
-    bool valid = true;
-    if constexpr (EDGE && !RDN_H16_EDGE_POST) valid = in_range(pos0 + NR * n + (lane & 15), tl.L);
+    constexpr bool valid = true;             // rows outside [0, L): zero_outside after the loop
     if constexpr (EPI == STAGE) {
       stg->put(n, __builtin_shufflevector(a.v[0], a.v[1], 0, 1, 2, 3, 4, 5, 6, 7));
       return;
@@ -555,7 +426,6 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     }
     store_slot(p, v, valid);
   };
-#endif
 
   Acc prev;
   constexpr int PF = RDN_H16_PF;       // B fragments in flight ahead of the step that consumes them
@@ -586,7 +456,7 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     prev = acc;
   }
   epilogue(NT - 1, prev);
-  if constexpr (EDGE && RDN_H16_EDGE_POST && EPI != STAGE) zero_outside(tl, dst, pos0 - tl.base, h, lane);
+  if constexpr (EDGE && EPI != STAGE) zero_outside(tl, dst, pos0 - tl.base, h, lane);
   tl.layer += 1;
 #if defined(RDN_ABLATE_NOBARRIER)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -632,11 +502,7 @@ __device__ __forceinline__ void head(Tile& tl, uint32_t src, const Frags& F, Fra
       const int k = KS * j + s, kp = k + PF;
       if (kp < K) B[kp % (PF + 1)] = *(const V*)(tl.lds + ba.at(ntile(kp / KS), kp % KS));
       if (live) {
-#if RDN_H16_M32
-        acc.v = mma(F.a[s], B[k % (PF + 1)], s == 0 ? __builtin_shufflevector(F.bias[0], F.bias[0], 0, 1, 2, 3, 0, 1, 2, 3, 0, 1, 2, 3, 0, 1, 2, 3) : acc.v);
-#else
         acc.v[0] = mma(F.a[s], B[k % (PF + 1)], s == 0 ? F.bias[0] : acc.v[0]);
-#endif
       }
       // the next layer's NLOAD operand loads spread over the head's K steps (operand i at step
       // i * K / NLOAD: every one is issued however few N-tiles the head has)
@@ -647,11 +513,7 @@ __device__ __forceinline__ void head(Tile& tl, uint32_t src, const Frags& F, Fra
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-#if RDN_H16_M32
-    out[j] = live ? acc.v[0] + acc.v[1] : 0.f;
-#else
     out[j] = acc.v[0][0] + acc.v[0][1];
-#endif
   }
   tl.layer += 1;
 }
@@ -671,21 +533,12 @@ __device__ __forceinline__ Tile init_tile(char* lds, const uint8_t* blob, const 
   tl.wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)tl.big, 0, 0x7fffffff, 0x00020000);
   tl.layer = 0;
   const int t = tid();
-#if RDN_H16_M32
-  const int e = (t & 63) >> 5;
-  tl.r0 = ((t >> 6) % RB) * RW + (t & 31);
-#pragma unroll
-  for (int d = -2; d <= 2; ++d)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) tl.koff[d + 2][v] = soff(tl.r0 + d, 2 * v + e);
-#else
   const int q = (t & 63) >> 4;
   tl.r0 = ((t >> 6) % RB) * RW + (t & 15);
 #pragma unroll
   for (int d = -2; d <= 2; ++d)
 #pragma unroll
     for (int u = 0; u < 2; ++u) tl.koff[d + 2][u] = soff(tl.r0 + d, 4 * u + q);
-#endif
   return tl;
 }
 

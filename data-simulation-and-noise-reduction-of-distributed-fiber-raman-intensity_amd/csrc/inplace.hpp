@@ -26,15 +26,6 @@ namespace ip {
 constexpr int MODE_F32 = 0, MODE_B1 = 1, MODE_X3 = 2, MODE_H8 = 3, MODE_F16 = 4;
 // single-plane 16-bit modes (one MFMA per product, one rounding per operand)
 __host__ __device__ constexpr bool single16(int mode) { return mode == MODE_B1 || mode == MODE_F16; }
-#ifndef RDN_IP_SPREAD_STORE
-#define RDN_IP_SPREAD_STORE 1
-#endif
-#ifndef RDN_IP_NTPIPE
-#define RDN_IP_NTPIPE 1
-#endif
-#ifndef RDN_IP_HIBASE
-#define RDN_IP_HIBASE 1
-#endif
 constexpr uint32_t LDS_BYTES = ACT_BYTES_F32;                    // 132096 (512 rows + guards)
 
 // Tile geometry by number of 128-row blocks: NBK = 4 -> 512 rows with 2 zero guard rows per side
@@ -242,18 +233,11 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4v __attribute__((ext_vector_type(4)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
-#ifndef RDN_H8_FASTSPLIT
-#define RDN_H8_FASTSPLIT 1
-#endif
 // 4 floats -> 4 e4m3 bytes of v / div (v_cvt_scalef32_pk_fp8_f32: the division is free)
 __device__ __forceinline__ uint32_t pk_e4m3_div(f32x4 v, float div) {
-#if RDN_H8_FASTSPLIT
   // both halves are overwritten: seed the tied destination with a source that dies here (v[0]),
   // so no zero-initialising v_mov is needed
   s16x2 o = __builtin_bit_cast(s16x2, v[0]);
-#else
-  s16x2 o = {0, 0};
-#endif
   o = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(o, v[0], v[1], div, false);
   o = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(o, v[2], v[3], div, true);
   return __builtin_bit_cast(uint32_t, o);
@@ -295,7 +279,6 @@ struct H8Split {
 };
 __device__ __forceinline__ H8Split h8_split(f32x4 r) {
   const f16x4 h = __builtin_convertvector(r, f16x4);
-#if RDN_H8_FASTSPLIT
   // lo = r - f32(h) in one v_fma_mix_f32 per value (f16 source operand, exact), and the e4m3 copy
   // of hi converted from r itself (its 3-bit mantissa cannot tell r from f16(r) except at
   // double-rounding ties): no f16 -> f32 round trip.  14 VALU per 4 values instead of 18.
@@ -308,10 +291,6 @@ __device__ __forceinline__ H8Split h8_split(f32x4 r) {
   asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo[2]) : "v"(hb.y), "v"(r[2]));
   asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(lo[3]) : "v"(hb.y), "v"(r[3]));
   return H8Split{h, pk_e4m3_div(r, H8_HI_DIV), pk_e4m3_div(lo, H8_LO_DIV)};
-#else
-  const f32x4 g = __builtin_convertvector(h, f32x4);
-  return H8Split{h, pk_e4m3_div(g, H8_HI_DIV), pk_e4m3_div(r - g, H8_LO_DIV)};
-#endif
 }
 
 template <> struct LayerBytes<MODE_H8> {
@@ -674,7 +653,6 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   constexpr bool COMP = MODE == MODE_F32 && RDN_F32_COMP && S == 0;   // S = 0: compensated chunks (two_sum)
   constexpr int CH = RDN_F32_CHUNK;
   constexpr int SP = COMP ? 1 : S;                           // MFMA accumulator sets
-  static_assert(!COMP || RDN_IP_NTPIPE, "compensated accumulation is implemented on the N-tile pipeline");
   f32x4 bias_l[MT];
   uint32_t sc_l[MT];
 #pragma unroll
@@ -704,7 +682,6 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
         blast[s][p] = pl * ROWB_F32 + ((O::bslot(2 * TS + s, q, p) ^ swz256(pl)) << 4);
       }
   }
-#if RDN_IP_HIBASE
   // a second set of B addresses 64 KiB up: blocks 2 and 3 then fit the 16-bit ds_read offset
   // (no v_add per read); block 4 still adds
   uint32_t badr2[O::KSTEPS][O::PLANES];
@@ -715,7 +692,6 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
       badr2[s][p] = badr[s][p] + 2 * BR * ROWB_F32;
       asm volatile("" : "+v"(badr2[s][p]));         // a register of its own, not re-derived per read
     }
-#endif
   auto ldb = [&](const uint32_t (&ad)[O::PLANES], uint32_t off) -> typename O::B {
     if constexpr (MODE == MODE_H8) return O::load_b_at(tl.lds, ad, off, cin);
     else return O::load_b_at(tl.lds, ad, off);
@@ -723,9 +699,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   auto read_b = [&](int j, int s, int i) -> typename O::B {
     if (TG::WRAP && j == 0 && s < TS && i == 0) return ldb(bfirst[s], 0);
     if (TG::WRAP && j == NB - 1 && s >= 2 * TS && i == NT - 1) return ldb(blast[s - 2 * TS], 0);
-#if RDN_IP_HIBASE
     if (j >= 2) return ldb(badr2[s], (uint32_t)(BR * (j - 2) + 16 * i) * ROWB_F32);
-#endif
     return ldb(badr[s], (uint32_t)(BR * j + 16 * i) * ROWB_F32);
   };
 #pragma unroll
@@ -843,7 +817,6 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #pragma unroll
       for (int mm = 0; mm < MT; ++mm) a.bias[mm] = load_bias<MODE>(wnext, MT * mp + mm), a.sc[mm] = load_scale<MODE>(wnext, MT * mp + mm);
     }
-#if RDN_IP_NTPIPE
     // B fragments rotate per N-tile: the reads of N-tile i for the next k-step (or for k-step 0 of
     // block j+1) are issued as soon as its MFMAs of this k-step are issued, so they fly under the
     // MFMAs of the other N-tile(s) instead of trailing the whole k-step -- same VGPRs as one set.
@@ -897,65 +870,6 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-#else
-#pragma unroll
-    for (int s = 0; s < O::KSTEPS; ++s) {
-      typename O::B bcur[NT];
-#pragma unroll
-      for (int i = 0; i < NT; ++i) bcur[i] = bnext[i];
-      if (s + 1 < O::KSTEPS) {
-#pragma unroll
-        for (int i = 0; i < NT; ++i) {
-#if defined(RDN_ABLATE_NOLDS)          // diagnostic builds only (tools/ablate.py): reuse block reads
-          bnext[i] = bcur[i];
-          asm volatile("" : "+v"(reinterpret_cast<f32x4&>(bnext[i])) ::);
-#else
-          bnext[i] = read_b(j, s + 1, i);
-#endif
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < NT; ++i) {
-        const typename O::B& b = bcur[i];
-#pragma unroll
-        for (int mm = 0; mm < MT; ++mm) {
-#if defined(RDN_ABLATE_NOMFMA)
-          part[s % SP][i][mm] += *(const f32x4*)&b;
-#else
-          part[s % SP][i][mm] = O::mma(a[mm][s], b, part[s % SP][i][mm], sc_l[mm], s);
-#endif
-        }
-      }
-      if (j == NB - 1 && has_next) {                                   // last use of a[.][s]
-#pragma unroll
-        for (int mm = 0; mm < MT; ++mm) a[mm][s] = O::load_a(wnext, MT * mp + mm, s, lane);
-      }
-#if RDN_IP_SPREAD_STORE
-      // lagged write-back of block j-2, one (N-tile, M-tile) piece per k-step: the LDS write
-      // bursts of the 8 waves spread over the block instead of landing on its first k-step
-      // (MODE_H8: one N-tile's M-tile pair per k-step)
-      if (j >= 2) {
-        constexpr int NP = NT * MT;
-        if constexpr (MODE == MODE_H8) {
-          if (s < NT) store_pair(j - 2, s);
-        } else if constexpr (O::KSTEPS >= NP) {
-          if (s < NP) store_piece(j - 2, s / MT, s % MT);
-        } else {
-#pragma unroll
-          for (int pc = s * NP / O::KSTEPS; pc < (s + 1) * NP / O::KSTEPS; ++pc) store_piece(j - 2, pc / MT, pc % MT);
-        }
-      }
-#else
-      if (s == 0 && j >= 2) store_block(j - 2);                        // lagged write-back
-#endif
-      // keep B-fragment reads within their k-step (VGPR budget of 2 waves/SIMD)
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (j + 1 < NB) {
-#pragma unroll
-      for (int i = 0; i < NT; ++i) bnext[i] = read_b(j + 1, 0, i);
-    }
-#endif
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll

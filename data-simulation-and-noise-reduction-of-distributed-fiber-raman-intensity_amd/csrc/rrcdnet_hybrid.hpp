@@ -2,35 +2,9 @@
 // RDN_F16MIX RRCDNet hybrid body, included by fused_inplace.hip once per tile length: PPNS names the
 // ping-pong engine instantiation (fused16.hpp: h16x, 640 rows; h16xs, 256 rows) and HNBK the in-place
 // tile's 128-row blocks (5 / 2) of the same length.
-// ping-pong buffer `src` (WB rows x 128 B, fused16 slot swizzle) -> the f16 plane of the in-place
-// tile (WB rows x 256 B, off_f32 swizzle).  The two overlap: everything is read before anything
-// is written.
-__device__ __forceinline__ void pingpong_to_tile(char* lds, uint32_t src) {
-  constexpr int ITEMS = PPNS::WB * 8 / THREADS;          // 10 (row, slot) items per thread
-  static_assert(PPNS::WB * 8 % THREADS == 0 && PPNS::WB == TileGeo<HNBK>::WB, "one tile length for both engines");
-  const int t = opaque_tid();
-  f16x8 v[ITEMS];
-#pragma unroll
-  for (int i = 0; i < ITEMS; ++i) {
-    const int item = t + THREADS * i, row = item >> 3, slot = item & 7;
-    v[i] = *(const f16x8*)(lds + src + PPNS::soff(row, slot));
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < ITEMS; ++i) {
-    const int item = t + THREADS * i, row = item >> 3, slot = item & 7;
-    *(f16x8*)(lds + off_f32(row, 16 * slot)) = v[i];
-  }
-  __syncthreads();
-}
-
-// RDN_F16MIX_STAGE=1: the producer of the corrected tail (the layer before it, which writes the e4m3
-// planes) runs on the ping-pong engine with its outputs staged in VGPRs as the in-place tile's three
-// planes and written after the layer's barrier -- no in-place plain layer and no conversion pass;
-// 0: the ping-pong buffer is converted (pingpong_to_tile) and that layer runs on the in-place engine
-#ifndef RDN_F16MIX_STAGE
-#define RDN_F16MIX_STAGE 1
-#endif
+// The producer of the corrected tail (the layer before it, which writes the e4m3 planes) runs on the
+// ping-pong engine with its outputs staged in VGPRs as the in-place tile's three planes and written
+// after the layer's barrier: no in-place plain layer and no conversion pass (+1 %, bit-equal).
 
 // the staged outputs of one ping-pong layer as the in-place H8 row planes: lane (w, q, c16) holds
 // N-tile n's row (w % RB) * RW + 16 n + c16 at 16-B slot 4 (w / RB) + q -- the f16 slot, and the
@@ -98,7 +72,6 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   }
   f32x4 id[16 * NBK / 4];
   LayerA<MODE_H8> a;
-#if RDN_F16MIX_STAGE
   // layers 0 .. PP - 1 plain, layer PP (the tail's producer) staged into the in-place planes
   for (int i = 0; i < PP / 2; ++i) {
     PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1);
@@ -118,26 +91,6 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   tl.layer = PP + 1;
   load_layer_a<MODE_H8>(tl, PP + 1, a);
   __syncthreads();
-#else
-  for (int i = 0; i < (PP - 1) / 2; ++i) {
-    PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1);
-    PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF1, PPNS::BUF0, 1, F1, F0);
-  }
-  // the last ping-pong layer (no next-layer operands: the in-place engine loads its own)
-  uint32_t cur;
-  if constexpr (PP % 2 == 1) {
-    PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1, false);
-    cur = PPNS::BUF1;
-  } else {
-    PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1);
-    PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF1, PPNS::BUF0, 1, F1, F0, false);
-    cur = PPNS::BUF0;
-  }
-  tl.layer = PP;
-  load_layer_a<MODE_H8>(tl, PP, a);
-  pingpong_to_tile(tl.lds, cur);
-  conv<MODE_H8, RELU, 1, EDGE, NBK, false, true, true>(tl, 1, id, a, true);       // writes the e4m3 planes
-#endif
   for (int i = 0; i < TAIL; ++i) conv<MODE_H8, RELU, 1, EDGE, NBK, true, true, true>(tl, 1, id, a, i + 1 < TAIL);
   double r[HO::ROWS];
   head<MODE_H8, NBK>(tl, 2, r);

@@ -17,24 +17,10 @@ CSRC = os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fi
 OUT = os.path.join(ROOT, "tools", "ablate_build")
 VARIANTS = {"base": "", "prev": "", "nolds": "-DRDN_ABLATE_NOLDS",
             "nomfma": "-DRDN_ABLATE_NOMFMA", "nostore": "-DRDN_ABLATE_NOSTORE", "noaload": "-DRDN_ABLATE_NOALOAD",
-            "pf3": "-DRDN_H16_PF=3", "ieee": "", "nospread": "-DRDN_IP_SPREAD_STORE=0", "prio": "-DRDN_IP_PRIO=1",
-            "prionospread": "-DRDN_IP_PRIO=1 -DRDN_IP_SPREAD_STORE=0", "stamps": "-DRDN_TEAM_STAMPS=1",
-            "stamps_pre0": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_ID_PRE=0", "stamps_reload": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_RELOAD_A=1",
-            "stamps_pre16": "-DRDN_TEAM_STAMPS=1 -DRDN_CBAM_ID_PRE=16", "nobar": "-DRDN_ABLATE_NOBARRIER",
-            "ntpipe": "-DRDN_IP_NTPIPE=1", "ntpipe0": "-DRDN_IP_NTPIPE=0", "fastsplit": "-DRDN_H8_FASTSPLIT=1",
-            "hibase0": "-DRDN_IP_HIBASE=0", "dsdn3": "-DRDN_DSDN_NBK=3", "comp0": "-DRDN_F32_COMP=0",
+            "pf3": "-DRDN_H16_PF=3", "ieee": "", "stamps": "-DRDN_TEAM_STAMPS=1", "nobar": "-DRDN_ABLATE_NOBARRIER", "dsdn3": "-DRDN_DSDN_NBK=3", "comp0": "-DRDN_F32_COMP=0",
             "chunk1": "-DRDN_F32_CHUNK=1", "chunk3": "-DRDN_F32_CHUNK=3", "chunk4": "-DRDN_F32_CHUNK=4",
-            "h16f16": "-DRDN_H16_F16=1", "h8plain": "-DRDN_ABLATE_H8_PLAIN", "nohead": "-DRDN_ABLATE_NOHEAD",
-            "mixold": "-DRDN_F16MIX_HYBRID=0", "pkrelu0": "-DRDN_H16_PKRELU=0", "ld2": "-DRDN_H16_LDSTEP=2", "ld4": "-DRDN_H16_LDSTEP=4", "m32": "-DRDN_H16_M32=1",
-            "m32ld2": "-DRDN_H16_M32=1 -DRDN_H16_LDSTEP=2", "m32pf2": "-DRDN_H16_M32=1 -DRDN_H16_PF=2",
-            "ord": "-DRDN_H16_LDORDER=1", "ordld3": "-DRDN_H16_LDORDER=1 -DRDN_H16_LDSTEP=3", "ordld2": "-DRDN_H16_LDORDER=1 -DRDN_H16_LDSTEP=2",
-            "wsame": "-DRDN_ABLATE_WSAME", "whalf": "-DRDN_ABLATE_WHALF",
-            "sleep1": "-DRDN_TEAM_SLEEP=1", "sleep2": "-DRDN_TEAM_SLEEP=2", "untag": "-DRDN_T16_TAGGED=0",
-            "untag_stamps": "-DRDN_T16_TAGGED=0 -DRDN_TEAM_STAMPS=1", "sleep4": "-DRDN_TEAM_SLEEP=4",
-            "saglobal": "-DRDN_T16_SA_LOCAL=0", "untag_saglobal": "-DRDN_T16_TAGGED=0 -DRDN_T16_SA_LOCAL=0", "salocal": "-DRDN_T16_SA_LOCAL=1", "pf2": "-DRDN_H16_PF=2", "pf4": "-DRDN_H16_PF=4", "edgesel": "-DRDN_H16_EDGE_POST=0", "alledge": "-DRDN_ABLATE_ALLEDGE -DRDN_TEAM_STAMPS=1",
-            "tail3": "-DRDN_F16MIX_TAIL=3", "tail4": "-DRDN_F16MIX_TAIL=4", "tail5": "-DRDN_F16MIX_TAIL=5",
-            "r02": "-DRDN_T16_TAGGED=0 -DRDN_T16_SA_LOCAL=0 -DRDN_TEAM_STAMPS=1",
-            "meanvalu": "-DRDN_T16_MEAN_MFMA=0", "sa1": "-DRDN_T16_SA_PAIR=0", "nostage": "-DRDN_F16MIX_STAGE=0", "nowin": "-DRDN_F16MIX_WIN=0", "mlp0": "-DRDN_T16_MLP_BFLY=0", "per2": "-DRDN_T16_POLL_PER=2", "sleep0": "-DRDN_TEAM_SLEEP=0", "sleep1": "-DRDN_TEAM_SLEEP=1", "sleep4": "-DRDN_TEAM_SLEEP=4", "nostem": "-DRDN_ABLATE_NOSTEM", "stem1": "-DRDN_H16_STEM2=0", "stem2a": "-DRDN_H16_STEM2=1", "noheadv": "-DRDN_ABLATE_NOHEADV",
+            "h16f16": "-DRDN_H16_F16=1", "h8plain": "-DRDN_ABLATE_H8_PLAIN", "nohead": "-DRDN_ABLATE_NOHEAD", "ld2": "-DRDN_H16_LDSTEP=2", "ld4": "-DRDN_H16_LDSTEP=4", "pf2": "-DRDN_H16_PF=2", "pf4": "-DRDN_H16_PF=4", "alledge": "-DRDN_ABLATE_ALLEDGE -DRDN_TEAM_STAMPS=1",
+            "tail3": "-DRDN_F16MIX_TAIL=3", "tail4": "-DRDN_F16MIX_TAIL=4", "tail5": "-DRDN_F16MIX_TAIL=5", "nowin": "-DRDN_F16MIX_WIN=0", "nostem": "-DRDN_ABLATE_NOSTEM", "noheadv": "-DRDN_ABLATE_NOHEADV",
             "tail0": "-DRDN_F16MIX_TAIL=0", "tail2": "-DRDN_F16MIX_TAIL=2"}
 
 
