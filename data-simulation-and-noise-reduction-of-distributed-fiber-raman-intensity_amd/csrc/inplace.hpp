@@ -475,6 +475,44 @@ __device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[Hea
 #pragma unroll
       for (int i = 0; i < 16; ++i) wv[t][i] = hwv[3 * chan(4 * (i >> 3) + q, i & 7) + t];
     const float bias = hw[192];
+    if constexpr (MODE == MODE_H8) {
+      // f16 plane by v_fma_mix_f32 (the f16 operand converted inside the FMA), e4m3-lo plane into a
+      // separate packed accumulator (v_pk_fma_f32 on the pairs v_cvt_pk_f32_fp8 returns), scaled by
+      // H8_LO_DIV (a power of two) once per row: 16 VALU per 8 values instead of ~28
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int k = 0; k < NBK; ++k) {
+        float acc = 0.f;
+        f32x2 accl = {0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const int pr = TG::row(128 * k + 16 * w + c16 + t - 1);
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int sl = 4 * u + q;
+            const u32x4 h = *(const u32x4*)(tl.lds + off_f32(pr, 16 * sl));
+            const u32x2 lo = *(const u32x2*)(tl.lds + off_f32(pr, 192 + 8 * sl));
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+              asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(acc) : "v"(h[d]), "v"(wv[t][8 * u + 2 * d]));
+              asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+                  : "+v"(acc) : "v"(h[d]), "v"(wv[t][8 * u + 2 * d + 1]));
+            }
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const f32x2 l0 = __builtin_amdgcn_cvt_pk_f32_fp8((int)lo[e], false);
+              const f32x2 l1 = __builtin_amdgcn_cvt_pk_f32_fp8((int)lo[e], true);
+              accl = __builtin_elementwise_fma(f32x2{wv[t][8 * u + 4 * e], wv[t][8 * u + 4 * e + 1]}, l0, accl);
+              accl = __builtin_elementwise_fma(f32x2{wv[t][8 * u + 4 * e + 2], wv[t][8 * u + 4 * e + 3]}, l1, accl);
+            }
+          }
+        }
+        acc = fmaf(accl[0] + accl[1], H8_LO_DIV, acc);
+        out[k] = (double)quarter_sum(acc) + (double)bias;
+      }
+    } else {
 #pragma unroll
     for (int k = 0; k < NBK; ++k) {
       float acc = 0.f;
@@ -485,13 +523,7 @@ __device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[Hea
         for (int u = 0; u < 2; ++u) {
           const int sl = 4 * u + q;
           f32x4 v0, v1;
-          if constexpr (MODE == MODE_H8) {
-            const f16x8 h = *(const f16x8*)(tl.lds + off_f32(pr, 16 * sl));
-            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-            const u32x2 lo = *(const u32x2*)(tl.lds + off_f32(pr, 192 + 8 * sl));
-            v0 = __builtin_convertvector(__builtin_shufflevector(h, h, 0, 1, 2, 3), f32x4) + unpk_e4m3(lo.x) * H8_LO_DIV;
-            v1 = __builtin_convertvector(__builtin_shufflevector(h, h, 4, 5, 6, 7), f32x4) + unpk_e4m3(lo.y) * H8_LO_DIV;
-          } else {
+          {
             typedef typename Op<MODE>::V8 V8;
             const V8 h = *(const V8*)(tl.lds + off_f32(pr, 16 * sl));
             v0 = __builtin_convertvector(__builtin_shufflevector(h, h, 0, 1, 2, 3), f32x4);
@@ -505,6 +537,7 @@ __device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[Hea
         }
       }
       out[k] = (double)quarter_sum(acc) + (double)bias;
+    }
     }
   } else {
     static_assert(TG::WB <= HEAD_ROWS * THREADS, "head rows per thread");

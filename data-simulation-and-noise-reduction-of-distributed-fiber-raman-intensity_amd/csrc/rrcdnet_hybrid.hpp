@@ -43,6 +43,36 @@ struct H8Stage {
   }
 };
 
+// Diagnostic builds (tools/hyb_stamps.py, -DRDN_HYB_STAMPS=1): s_memtime at the phase boundaries of
+// the hybrid body, summed over workgroups into the range workspace behind its status word (u64
+// [1 + phase], [9] = workgroups).  In the product build every stamp compiles to nothing.
+#ifndef RDN_HYB_STAMPS
+#define RDN_HYB_STAMPS 0
+#endif
+struct HybStamps {
+  unsigned long long t, acc[8];
+  __device__ __forceinline__ HybStamps() {
+    if (RDN_HYB_STAMPS) {
+      for (int k = 0; k < 8; ++k) acc[k] = 0;
+      t = __builtin_amdgcn_s_memtime();
+    }
+  }
+  __device__ __forceinline__ void operator()(int k) {
+    if (RDN_HYB_STAMPS) {
+      const unsigned long long n = __builtin_amdgcn_s_memtime();
+      acc[k] += n - t;
+      t = n;
+    }
+  }
+  __device__ __forceinline__ void flush(unsigned* status) {
+    if (RDN_HYB_STAMPS && status && __builtin_amdgcn_workitem_id_x() == 0) {
+      unsigned long long* w = (unsigned long long*)status;
+      for (int k = 0; k < 8; ++k) atomicAdd(w + 1 + k, acc[k]);
+      atomicAdd(w + 9, 1ull);
+    }
+  }
+};
+
 // Returns false, having written nothing, when the tile's input window leaves [F16MIX_WIN_LO,
 // F16MIX_WIN_HI] (common.hpp): the caller then runs the all-corrected body on the tile.
 template <bool EDGE, int TAIL>
@@ -50,6 +80,7 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
                                                     int L, int T, int tiles, unsigned* status) {
   constexpr int H = fused_halo(RRCDNET), NBK = HNBK, PP = 14 - TAIL;   // ping-pong layers of the right branch
   using HO = HeadOut<MODE_H8, NBK>;
+  HybStamps st;
   int n16;
   PPNS::Tile t16 = PPNS::make_tile(tl.lds, blob, x, L, T, tiles, H, n16);
   PPNS::Frags F0, F1;            // alternating operand buffers (fused16.hpp layer)
@@ -70,6 +101,7 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
     __syncthreads();
     if (spiked) return false;
   }
+  st(0);
   f32x4 id[16 * NBK / 4];
   LayerA<MODE_H8> a;
   // layers 0 .. PP - 1 plain, layer PP (the tail's producer) staged into the in-place planes
@@ -91,7 +123,9 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   tl.layer = PP + 1;
   load_layer_a<MODE_H8>(tl, PP + 1, a);
   __syncthreads();
+  st(1);
   for (int i = 0; i < TAIL; ++i) conv<MODE_H8, RELU, 1, EDGE, NBK, true, true, true>(tl, 1, id, a, i + 1 < TAIL);
+  st(2);
   double r[HO::ROWS];
   head<MODE_H8, NBK>(tl, 2, r);
   park_rows<MODE_H8, NBK>(tl, y, n, r, H, T);
@@ -101,12 +135,15 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   t16.layer = 15;
   PPNS::load_frags(t16, 15, F0);
   __syncthreads();               // the left stem overwrites the rows the right head just read
+  st(3);
   PPNS::stem(t16, 1, PPNS::BUF0);
   PPNS::lds_barrier();
+  st(4);
   for (int i = 0; i < 7; ++i) {  // left layers 15-28 (the one at 22 with d = 1)
     PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 2, F0, F1);
     PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF1, PPNS::BUF0, 2 * i + 1 == 7 ? 1 : 2, F1, F0);
   }
+  st(5);
   float l[PPNS::HN];
   PPNS::head<EDGE>(t16, PPNS::BUF0, F0, F1, false, l);
   // hand the left head's rows (ping-pong lane layout) to the right head's (HeadOut) through LDS
@@ -130,6 +167,8 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   }
   if (sat) nan_rows(o);
   store_out<MODE_H8, NBK>(tl, y, n, o, H, T);
+  st(6);
+  st.flush(status);
   return true;
 }
 

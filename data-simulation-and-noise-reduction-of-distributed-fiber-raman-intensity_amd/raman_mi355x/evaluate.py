@@ -25,7 +25,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import engine
+from . import _lib, engine
 from .distributed import shard, world
 
 KEYS = ("MSE", "SSIM", "Smoothness", "Peak2Peak")
@@ -74,6 +74,25 @@ def _model_forward(model, x, ws):
                           workspace=ws)
 
 
+def _gate(model, device):
+    """Device running max of |input| for an engine module in a 16-bit mode (models.INPUT_GATE)."""
+    if not _engine_module(model) or model.engine_code == 0:
+        return None
+    return torch.zeros((), dtype=torch.float32, device=device)
+
+
+def _track(gate, x):
+    lo, hi = torch.aminmax(x)                      # one pass, no |x| copy
+    torch.maximum(gate, torch.maximum(-lo, hi), out=gate)
+
+
+def _check_gate(model, gate):
+    from .models import INPUT_GATE
+    if gate is not None and float(gate) > INPUT_GATE:
+        raise _lib.RangeError(f"evaluate: |input| reached {float(gate):.3g}, beyond the 16-bit modes' domain "
+                              f"({INPUT_GATE}, normalised intensity); evaluate this data in 'fp32'")
+
+
 def _workspace(model, n, L, device):
     if (not _engine_module(model) or not engine.needs_workspace(model.ARCH, model.engine_code)
             or torch.device(device).type != "cuda"):
@@ -100,15 +119,19 @@ def evaluate(model, noisy_data, clean_data, batch_size=1024, device=None):
     # fp64 clean stays fp64 (the metrics compare against the same float64 values as evaulate.py)
     cdt = torch.float64 if (clean.dtype == torch.float64 if torch.is_tensor(clean) else clean.dtype == np.float64) \
         else torch.float32
+    gate = _gate(model, device)
     with torch.no_grad():
         for b0 in range(lo, hi, batch_size):
             b1 = min(hi, b0 + batch_size)
             x = torch.as_tensor(noisy[b0:b1], dtype=torch.float32).to(device).unsqueeze(1)
             c = torch.as_tensor(clean[b0:b1], dtype=cdt).to(device)
             y = _model_forward(model, x, ws)
+            if gate is not None:
+                _track(gate, x)
             engine.metrics(y.squeeze(1), c, per_spectrum=False, acc=acc)
     if ws is not None:
         ws.check()
+    _check_gate(model, gate)
     _all_reduce_acc(acc)
     return means_from_acc(acc)
 
@@ -139,6 +162,7 @@ def evaluate_synthetic(models, total, seed=20250410, signal_length=10000, batch_
             model.eval()
             acc = engine.new_acc(device)
             ws = _workspace(model, B, L, device)
+            gate = _gate(model, device)
             packed = model.packed_weights(device)
             if dist.is_available() and dist.is_initialized():
                 dist.barrier()
@@ -157,9 +181,12 @@ def evaluate_synthetic(models, total, seed=20250410, signal_length=10000, batch_
                                 out=(clean[:nb], noisy[:nb]), **gen_kwargs)
                 engine.forward(model.ARCH, model.engine_code, packed, noisy[:nb].view(nb, 1, L), out=y[:nb],
                                check=False, workspace=ws)
+                if gate is not None:
+                    _track(gate, noisy[:nb])
                 engine.metrics(y[:nb].view(nb, L), clean[:nb], per_spectrum=False, acc=acc)
             if ws is not None:
-                ws.check()                  # waits for the stream; raises on a timed-out hand-off
+                ws.check()                  # waits for the stream; raises on a timed-out hand-off / range
+            _check_gate(model, gate)
             torch.cuda.synchronize(device)
             el = time.perf_counter() - t0
             t = torch.tensor([el], dtype=torch.float64)

@@ -42,6 +42,17 @@ _VERSION = operator.attrgetter("_version")
 _DATA_PTR = torch.Tensor.data_ptr
 
 C = 64
+# Input domain of the 16-bit modes: normalised intensity (数据集产生.py:38-40 min-max normalises the clean
+# signal to [0, 1]; noise and 5-15 sigma spikes keep every simulated spectrum inside [-1, 2]).  A
+# batch whose |x| exceeds INPUT_GATE runs in fp32 instead: beyond it the 16-bit arithmetic no longer
+# tracks the reference within the bar (the activations, and their absolute rounding error, scale with
+# the input; sigmoid heads turn that into output error -- tests/test_range_gpu.py).
+INPUT_GATE = 4.0
+
+
+def _absmax(x):
+    lo, hi = torch.aminmax(x)                     # one pass, no |x| copy; syncs the stream
+    return max(-float(lo), float(hi))
 
 
 def _conv(cin=C, cout=C, dilation=1, bias=True, k=3):
@@ -169,17 +180,23 @@ class _EngineNet(nn.Module):
             raise ValueError(f"{type(self).__name__}: expected input (N, 1, L), got {tuple(x.shape)}")
         if x.dtype != torch.float32:
             raise TypeError(f"{type(self).__name__}: expected float32 input, got {x.dtype}")
+        code = self._engine_code
+        why = None
         try:
-            return engine.forward(self.ARCH, self._engine_code, self.packed_weights(x.device), x,
-                                  workspace=self._workspace(x))
+            y = engine.forward(self.ARCH, code, self.packed_weights(x.device), x, workspace=self._workspace(x))
         except _lib.RangeError:
-            # an activation left the e4m3 planes' range (inputs far beyond normalised intensity):
-            # never return the NaN tiles -- the batch is re-run in exact fp32, which has no such bound
-            if not self._range_warned:
-                warnings.warn(f"{type(self).__name__}: activations beyond the '{self._engine_dtype}' range "
-                              "(|v| > 1792); this batch ran in fp32 instead", RuntimeWarning, stacklevel=2)
-                self._range_warned = True
-            return engine.forward(self.ARCH, 0, self._fp32_weights(x.device), x)
+            # an activation left the e4m3 planes' range: never return the NaN tiles
+            why = "activations beyond the e4m3 planes' range (|v| > 1792)"
+        if why is None and code != 0 and x.numel() and _absmax(x) > INPUT_GATE:
+            why = f"|input| beyond {INPUT_GATE} (outside normalised intensity)"
+        if why is None:
+            return y
+        # the batch is re-run in exact fp32, which has neither bound
+        if not self._range_warned:
+            warnings.warn(f"{type(self).__name__} '{self._engine_dtype}': {why}; this batch ran in fp32 instead",
+                          RuntimeWarning, stacklevel=2)
+            self._range_warned = True
+        return engine.forward(self.ARCH, 0, self._fp32_weights(x.device), x)
 
 
 def _check_defaults(name, in_channels, num_res_blocks):

@@ -88,14 +88,23 @@ def test_heldout_plain_f16_is_outside_the_bar_the_mix_fixes(which):
 
 @pytest.mark.parametrize("which", list(SETS))
 def test_heldout_fp32_matches_reference(which):
+    """fp32 within 1e-5 max-relative of the exact (float64) reference forward, and of the fp32 reference
+    to 1e-5 plus the fp32 reference's own distance from exact: on the 200-epoch RRCDNet (heldout2) the
+    reference's fp32 CPU forward is itself 1.5e-5 from exact, so 1e-5 of IT is not a property any
+    other fp32 summation order can have."""
     g, sd = _heldout(which)
     m = _model(sd, "fp32")
     for name in ("main", "odd"):
-        ref = g[f"ref_{name}"]
+        ref, ex = g[f"ref_{name}"], g[f"f64_{name}"]
         y = _run(m, g[f"in_{name}"])
-        rel = float(np.abs(y - ref).max() / np.abs(ref).max())
-        print(f"heldout/{name}: fp32 max-rel {rel:.2e}")
-        assert rel <= F32_REL
+        sc = float(np.abs(ex).max())
+        rel64 = float(np.abs(y - ex).max()) / sc
+        rel = float(np.abs(y - ref).max()) / sc
+        ref_own = float(np.abs(ref - ex).max()) / sc
+        print(f"{which}/{name}: fp32 max-rel {rel:.2e} vs the fp32 reference, {rel64:.2e} vs exact "
+              f"(the reference itself {ref_own:.2e} from exact)")
+        assert rel64 <= F32_REL
+        assert rel <= F32_REL + ref_own
 
 
 def test_heldout2_config1_thousand_spectra():

@@ -1,0 +1,68 @@
+"""Phase costs of the RDN_F16MIX hybrid (diagnostic, not part of the product): the `hybstamps` build of
+tools/ablate.py (-DRDN_HYB_STAMPS=1, rrcdnet_hybrid.hpp HybStamps) sums s_memtime deltas per phase over
+the full tiles' workgroups into the range workspace.
+
+    python tools/ablate.py build hybstamps     # build container
+    python tools/hyb_stamps.py                 # GPU box: 2048 simulator spectra, random-init RRCDNet
+"""
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fiber-raman-intensity_amd"))
+PHASES = ["right stem + window vote", "right ping-pong layers 0-9 (9 staged)", "in-place corrected tail (5)",
+          "right head + park", "left stem", "left layers 15-28 (14)", "left head + vote + combine + store"]
+PER_LAYER = {1: 10, 2: 5, 5: 14}
+
+
+def main():
+    import raman_mi355x as R
+    from raman_mi355x import _lib, engine
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "ablate_build", f"lib_{sys.argv[1] if len(sys.argv) > 1 else 'hybstamps'}.so"))
+    for fn, (args, res) in _lib._SIGNATURES.items():
+        if hasattr(lib, fn):
+            getattr(lib, fn).argtypes, getattr(lib, fn).restype = args, res
+    dev = torch.device("cuda")
+    B, L = 2048, 10000
+    _, noisy, _, _ = engine.generate(B, 1, signal_length=L, device=dev)
+    torch.manual_seed(0)
+    model = R.RRCDNet()
+    names = engine.param_names("RRCDNet")
+    sd = model.state_dict()
+    host = [sd[k].detach().float().contiguous() for k in names]
+    ptrs = (ctypes.c_void_p * len(host))(*[t.data_ptr() for t in host])
+    numels = (ctypes.c_int64 * len(host))(*[t.numel() for t in host])
+    size = ctypes.c_size_t()
+    assert lib.rdn_packed_size(1, 5, ctypes.byref(size)) == 0
+    blob = torch.empty(size.value, dtype=torch.uint8)
+    assert lib.rdn_pack(1, 5, ptrs, numels, len(host), ctypes.c_void_p(blob.data_ptr()), size.value) == 0
+    blob = blob.to(dev)
+    y = torch.empty_like(noisy)
+    ws = torch.zeros(256, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):                                  # warm-up
+        lib.rdn_forward(1, 5, blob.data_ptr(), noisy.data_ptr(), y.data_ptr(), B, L, ws.data_ptr(), 256, stream)
+    torch.cuda.synchronize()
+    ws.zero_()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        assert lib.rdn_forward(1, 5, blob.data_ptr(), noisy.data_ptr(), y.data_ptr(), B, L, ws.data_ptr(), 256, stream) == 0
+    e1.record()
+    torch.cuda.synchronize()
+    w = ws.view(torch.int64).cpu().tolist()
+    n = w[9]
+    tot = sum(w[1:8])
+    print(f"{e0.elapsed_time(e1) / 5:.2f} ms per forward of {B} spectra; {n} hybrid workgroups stamped; "
+          f"{tot / n:.0f} cycles per workgroup")
+    for k, name in enumerate(PHASES):
+        c = w[1 + k] / n
+        extra = f"  ({c / PER_LAYER[k]:.0f} per layer)" if k in PER_LAYER else ""
+        print(f"  {name:42s} {c:9.0f} cycles  {100 * w[1 + k] / tot:5.1f} %{extra}")
+
+
+if __name__ == "__main__":
+    main()
