@@ -206,8 +206,40 @@ __device__ __forceinline__ void mstep(const Frags& F, int s, V b, Acc& acc) {
 // (row, slot) item per lane and step waited on its loads ten times: 7 % of the RDN_F16MIX hybrid,
 // which runs two stems per tile); channel pairs on v_pk_fma_f32 and a packed ReLU after the rounding
 // (without ACCUM).
+// The stem's x values (rows lane + 64k, taps -1 / 0 / +1) fetched by buffer loads: positions outside
+// [0, L) read 0 by the range check of the resource.  A caller may issue them early (stem_load) and
+// hand them to the stem later, so their latency hides under other work (the RDN_F16MIX hybrid
+// fetches its left stem's inputs before the right head).
+constexpr int STEM_NK = WB / 64;
+struct StemX {
+  float xm[STEM_NK], x0[STEM_NK], xp[STEM_NK];
+};
+__device__ __forceinline__ StemX stem_load(const Tile& tl) {
+  StemX s;
+  const int lane = tid() & 63;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)tl.x, 0, tl.L * 4, 0x00020000);
+#pragma unroll
+  for (int k = 0; k < STEM_NK; ++k) {
+    const int p = tl.base + lane + 64 * k;
+    s.xm[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (p - 1), 0, 0));
+    s.x0[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * p, 0, 0));
+    s.xp[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (p + 1), 0, 0));
+  }
+  return s;
+}
+
+// Conv1d(1, 64, 3, padding=1) (+ folded BN) + ReLU in fp32.  ACCUM adds the result onto the resident
+// row (PIDN/train.py:105, identity recomputed from x).  out_lo / out_hi (lo <= hi): returns whether any
+// input this thread read at the tile's rows lies outside [lo, hi] (the RDN_F16MIX spiked-tile test,
+// rrcdnet_hybrid.hpp), else false.
+// Wave w computes slot w (8 channels, its 32 weights scalar-loaded once) for rows lane + 64k, and
+// every x value of those rows is fetched before the first is used -- one memory latency per stem (a
+// loop of one (row, slot) item per lane and step waited on its loads ten times: 7 % of the RDN_F16MIX
+// hybrid, which runs two stems per tile); channel pairs on v_pk_fma_f32 and a packed ReLU after the
+// rounding (without ACCUM).
 template <bool ACCUM = false>
-__device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, float out_lo = 1.f, float out_hi = 0.f) {
+__device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, const StemX& xs, float out_lo = 1.f,
+                                     float out_hi = 0.f) {
   const float* swp = tl.small + sslot * SMALL_SLOT_FLOATS;
   asm volatile("" : "+s"(swp));      // no reuse of scalar-loaded weights across the layers in between
   const cfloat* sw = (const cfloat*)swp;
@@ -216,17 +248,8 @@ __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, fl
   return outside;
 #endif
   static_assert(WB % 64 == 0 && WAVES == 8, "one slot per wave, rows lane + 64k");
-  constexpr int NK = WB / 64;
+  constexpr int NK = STEM_NK;
   const int g = __builtin_amdgcn_readfirstlane(tid() >> 6), lane = tid() & 63;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)tl.x, 0, tl.L * 4, 0x00020000);
-  float xm[NK], x0[NK], xp[NK];
-#pragma unroll
-  for (int k = 0; k < NK; ++k) {
-    const int p = tl.base + lane + 64 * k;
-    xm[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (p - 1), 0, 0));
-    x0[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * p, 0, 0));
-    xp[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (p + 1), 0, 0));
-  }
   float wb[8], wm[8], w0[8], wp[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -241,14 +264,14 @@ __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, fl
     const int row = lane + 64 * k;
     const int p = tl.base + row;
     const bool valid = in_range(p, tl.L);
-    if (out_lo <= out_hi) outside = outside || x0[k] < out_lo || x0[k] > out_hi;
+    if (out_lo <= out_hi) outside = outside || xs.x0[k] < out_lo || xs.x0[k] > out_hi;
     V* ptr = (V*)(tl.lds + dst + soff(row, g));
     V v;
     if (!ACCUM) {
       // channel pairs by v_pk_fma_f32 (each half one fmaf, same order), ReLU after the rounding
       // (rounding is monotone and keeps 0: the same value), rows outside [0, L) zeroed last
       typedef float f32x2 __attribute__((ext_vector_type(2)));
-      const f32x2 xm2 = {xm[k], xm[k]}, x02 = {x0[k], x0[k]}, xp2 = {xp[k], xp[k]};
+      const f32x2 xm2 = {xs.xm[k], xs.xm[k]}, x02 = {xs.x0[k], xs.x0[k]}, xp2 = {xs.xp[k], xs.xp[k]};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         f32x2 a = {wb[2 * q], wb[2 * q + 1]};
@@ -263,20 +286,24 @@ __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, fl
       *ptr = v;
       continue;
     }
-    if (ACCUM) v = *ptr;
+    v = *ptr;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float a = wb[j];
-      a = fmaf(wm[j], xm[k], a);
-      a = fmaf(w0[j], x0[k], a);
-      a = fmaf(wp[j], xp[k], a);
+      a = fmaf(wm[j], xs.xm[k], a);
+      a = fmaf(w0[j], xs.x0[k], a);
+      a = fmaf(wp[j], xs.xp[k], a);
       a = fmaxf(a, 0.f);
-      if (ACCUM) a += (float)v[j];
+      a += (float)v[j];
       v[j] = (E)(valid ? a : 0.f);
     }
     *ptr = v;
   }
   return outside;
+}
+template <bool ACCUM = false>
+__device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, float out_lo = 1.f, float out_hi = 0.f) {
+  return stem<ACCUM>(tl, sslot, dst, stem_load(tl), out_lo, out_hi);
 }
 
 enum Epi : int {

@@ -357,7 +357,11 @@ template <> struct Op<MODE_H8> {
   }
   __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc, uint32_t sa, int s) {
     const int sb = (__builtin_amdgcn_workitem_id_x() & 32) ? H8_LO_E8M0 : H8_HI_E8M0;   // lanes 32-63: the lo blocks
-#if !defined(RDN_ABLATE_H8_PLAIN)
+#if defined(RDN_ABLATE_F6)              // diagnostic (tools/ablate.py): the e2m3 MFMA's rate, wrong results
+    if (s == 0) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 2, 2, 0, (int)sa, 0, sb);
+    else if (s == 1) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 2, 2, 1, (int)sa, 0, sb);
+    else acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 2, 2, 2, (int)sa, 0, sb);
+#elif !defined(RDN_ABLATE_H8_PLAIN)
     if (s == 0) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 0, (int)sa, 0, sb);
     else if (s == 1) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 1, (int)sa, 0, sb);
     else acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 2, (int)sa, 0, sb);
@@ -456,8 +460,13 @@ __device__ __forceinline__ float quarter_sum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);                   // and the other 16-lane row
 }
 
-template <int MODE, int NBK = 4>
-__device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[HeadOut<MODE, NBK>::ROWS]) {
+struct NoPre {
+  __device__ void operator()() const {}
+};
+// pre(): issued right after the head's weight loads (a caller's prefetch that must not sit in front
+// of them in the vector-memory queue)
+template <int MODE, int NBK = 4, class Pre = NoPre>
+__device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[HeadOut<MODE, NBK>::ROWS], Pre pre = Pre{}) {
   using TG = TileGeo<NBK>;
   const cfloat* hw = small_slot(tl, slot);
   if constexpr (HeadOut<MODE, NBK>::VEC) {
@@ -475,43 +484,59 @@ __device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[Hea
 #pragma unroll
       for (int i = 0; i < 16; ++i) wv[t][i] = hwv[3 * chan(4 * (i >> 3) + q, i & 7) + t];
     const float bias = hw[192];
+    pre();
     if constexpr (MODE == MODE_H8) {
       // f16 plane by v_fma_mix_f32 (the f16 operand converted inside the FMA), e4m3-lo plane into a
       // separate packed accumulator (v_pk_fma_f32 on the pairs v_cvt_pk_f32_fp8 returns), scaled by
-      // H8_LO_DIV (a power of two) once per row: 16 VALU per 8 values instead of ~28
+      // H8_LO_DIV (a power of two) once per row.  The NBK rows of a lane are independent sums,
+      // interleaved innermost: one row's 48-term sum is a dependent FMA chain, and the head of a
+      // single chain per row waited on FMA latency (the hybrid's right head + park: 11.6k cycles per
+      // tile, tools/hyb_stamps.py)
       typedef float f32x2 __attribute__((ext_vector_type(2)));
       typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      float acc[NBK];
+      f32x2 accl[NBK];
 #pragma unroll
-      for (int k = 0; k < NBK; ++k) {
-        float acc = 0.f;
-        f32x2 accl = {0.f, 0.f};
+      for (int k = 0; k < NBK; ++k) acc[k] = 0.f, accl[k] = f32x2{0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {
-          const int pr = TG::row(128 * k + 16 * w + c16 + t - 1);
+      for (int t = 0; t < 3; ++t) {
 #pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int sl = 4 * u + q;
-            const u32x4 h = *(const u32x4*)(tl.lds + off_f32(pr, 16 * sl));
-            const u32x2 lo = *(const u32x2*)(tl.lds + off_f32(pr, 192 + 8 * sl));
+        for (int u = 0; u < 2; ++u) {
+          const int sl = 4 * u + q;
+          u32x4 h[NBK];
+          u32x2 lo[NBK];
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
-              asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(acc) : "v"(h[d]), "v"(wv[t][8 * u + 2 * d]));
+          for (int k = 0; k < NBK; ++k) {
+            const int pr = TG::row(128 * k + 16 * w + c16 + t - 1);
+            h[k] = *(const u32x4*)(tl.lds + off_f32(pr, 16 * sl));
+            lo[k] = *(const u32x2*)(tl.lds + off_f32(pr, 192 + 8 * sl));
+          }
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+#pragma unroll
+            for (int k = 0; k < NBK; ++k)
+              asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(acc[k]) : "v"(h[k][d]), "v"(wv[t][8 * u + 2 * d]));
+#pragma unroll
+            for (int k = 0; k < NBK; ++k)
               asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-                  : "+v"(acc) : "v"(h[d]), "v"(wv[t][8 * u + 2 * d + 1]));
-            }
+                  : "+v"(acc[k]) : "v"(h[k][d]), "v"(wv[t][8 * u + 2 * d + 1]));
+          }
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const f32x2 l0 = __builtin_amdgcn_cvt_pk_f32_fp8((int)lo[e], false);
-              const f32x2 l1 = __builtin_amdgcn_cvt_pk_f32_fp8((int)lo[e], true);
-              accl = __builtin_elementwise_fma(f32x2{wv[t][8 * u + 4 * e], wv[t][8 * u + 4 * e + 1]}, l0, accl);
-              accl = __builtin_elementwise_fma(f32x2{wv[t][8 * u + 4 * e + 2], wv[t][8 * u + 4 * e + 3]}, l1, accl);
+          for (int e = 0; e < 2; ++e) {
+#pragma unroll
+            for (int k = 0; k < NBK; ++k) {
+              const f32x2 l0 = __builtin_amdgcn_cvt_pk_f32_fp8((int)lo[k][e], false);
+              const f32x2 l1 = __builtin_amdgcn_cvt_pk_f32_fp8((int)lo[k][e], true);
+              accl[k] = __builtin_elementwise_fma(f32x2{wv[t][8 * u + 4 * e], wv[t][8 * u + 4 * e + 1]}, l0, accl[k]);
+              accl[k] = __builtin_elementwise_fma(f32x2{wv[t][8 * u + 4 * e + 2], wv[t][8 * u + 4 * e + 3]}, l1, accl[k]);
             }
           }
         }
-        acc = fmaf(accl[0] + accl[1], H8_LO_DIV, acc);
-        out[k] = (double)quarter_sum(acc) + (double)bias;
       }
+#pragma unroll
+      for (int k = 0; k < NBK; ++k)
+        out[k] = (double)quarter_sum(fmaf(accl[k][0] + accl[k][1], H8_LO_DIV, acc[k])) + (double)bias;
     } else {
 #pragma unroll
     for (int k = 0; k < NBK; ++k) {
@@ -944,9 +969,11 @@ __device__ __forceinline__ uint64_t corr_mask(const uint8_t* blob) {
   return (uint64_t)hi << 32 | lo;
 }
 
-__device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const float* x, int L, int T,
-                                          int tiles, int halo, int& n_out) {
-  const int n = __builtin_amdgcn_workgroup_id_x() / tiles, tile = __builtin_amdgcn_workgroup_id_x() - n * tiles;
+// tile `id` = (spectrum n, tile index within it) of a launch: workgroup `id` of a one-tile-per-workgroup
+// grid, or the persistent kernels' loop index
+__device__ __forceinline__ Tile make_tile_at(char* lds, const uint8_t* blob, const float* x, int L, int T, int tiles,
+                                             int halo, int64_t id, int& n_out) {
+  const int n = (int)(id / tiles), tile = (int)(id - (int64_t)n * tiles);
   n_out = n;
   Tile tl;
   tl.lds = lds;
@@ -959,6 +986,10 @@ __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const 
   tl.corr = corr_mask(blob);
   tl.amax = 0.f;
   return tl;
+}
+__device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const float* x, int L, int T,
+                                          int tiles, int halo, int& n_out) {
+  return make_tile_at(lds, blob, x, L, T, tiles, halo, __builtin_amdgcn_workgroup_id_x(), n_out);
 }
 
 // End-of-tile range vote of the MODE_H8 kernels (h8_track): whether any lane of the workgroup saw a

@@ -43,6 +43,10 @@ struct H8Stage {
   }
 };
 
+#ifndef RDN_HYB_PARK
+#define RDN_HYB_PARK 0
+#endif
+
 // Diagnostic builds (tools/hyb_stamps.py, -DRDN_HYB_STAMPS=1): s_memtime at the phase boundaries of
 // the hybrid body, summed over workgroups into the range workspace behind its status word (u64
 // [1 + phase], [9] = workgroups).  In the product build every stamp compiles to nothing.
@@ -73,22 +77,26 @@ struct HybStamps {
   }
 };
 
+// The ping-pong view of the same tile (rows [base, base + WB) of spectrum n).
+__device__ __forceinline__ PPNS::Tile pp_tile(const Tile& tl) {
+  return PPNS::init_tile(tl.lds, (const uint8_t*)tl.small, tl.big, tl.x, tl.L, tl.base);
+}
+
 // Returns false, having written nothing, when the tile's input window leaves [F16MIX_WIN_LO,
 // F16MIX_WIN_HI] (common.hpp): the caller then runs the all-corrected body on the tile.
 template <bool EDGE, int TAIL>
-__device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blob, const float* x, float* y, int n,
-                                                    int L, int T, int tiles, unsigned* status) {
+__device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, float* y, int n, int L, int T, unsigned* status) {
   constexpr int H = fused_halo(RRCDNET), NBK = HNBK, PP = 14 - TAIL;   // ping-pong layers of the right branch
   using HO = HeadOut<MODE_H8, NBK>;
   HybStamps st;
-  int n16;
-  PPNS::Tile t16 = PPNS::make_tile(tl.lds, blob, x, L, T, tiles, H, n16);
+  PPNS::Tile t16 = pp_tile(tl);
   PPNS::Frags F0, F1;            // alternating operand buffers (fused16.hpp layer)
   PPNS::load_frags(t16, 0, F0);
+  const PPNS::StemX xr = PPNS::stem_load(t16);
   {
     // the stem tests its inputs against the window; one word per wave at the end of the LDS (first
     // written by layer 0, after the barrier below and the read behind it)
-    const bool out = PPNS::stem(t16, 0, PPNS::BUF0, F16MIX_WIN_LO, F16MIX_WIN_HI);
+    const bool out = PPNS::stem(t16, 0, PPNS::BUF0, xr, F16MIX_WIN_LO, F16MIX_WIN_HI);
     unsigned* vote = (unsigned*)(tl.lds + PPNS::LDS_BYTES) - PPNS::WAVES;
     const bool wave_out = __builtin_amdgcn_ballot_w64(out) != 0;
     if ((PPNS::tid() & 63) == 0) vote[PPNS::tid() >> 6] = wave_out ? 1u : 0u;
@@ -126,9 +134,18 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   st(1);
   for (int i = 0; i < TAIL; ++i) conv<MODE_H8, RELU, 1, EDGE, NBK, true, true, true>(tl, 1, id, a, i + 1 < TAIL);
   st(2);
+  // the left stem's inputs, issued right behind the head's weight loads (not before them: a wait for
+  // the weights would wait for these too), so their latency hides under the head (the left stem
+  // waited on them: 6.2k cycles per tile, tools/hyb_stamps.py)
+  PPNS::StemX xl;
   double r[HO::ROWS];
-  head<MODE_H8, NBK>(tl, 2, r);
+  head<MODE_H8, NBK>(tl, 2, r, [&] { xl = PPNS::stem_load(t16); });
+#if RDN_HYB_PARK
   park_rows<MODE_H8, NBK>(tl, y, n, r, H, T);
+#else
+  float rk[HO::ROWS];            // the right head's rows, rounded as parking them in y would
+  round_rows(r, rk);
+#endif
   // left branch: layers 15-28 and the head on the ping-pong engine (f16 activations into the head,
   // whose weights carry their rounding residue: tools/head_fusion_emul.py puts this at 1.52e-2 on
   // trained RRCDNet against 1.44e-2 with the split head, the bar being 2e-2)
@@ -136,7 +153,7 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   PPNS::load_frags(t16, 15, F0);
   __syncthreads();               // the left stem overwrites the rows the right head just read
   st(3);
-  PPNS::stem(t16, 1, PPNS::BUF0);
+  PPNS::stem(t16, 1, PPNS::BUF0, xl);
   PPNS::lds_barrier();
   st(4);
   for (int i = 0; i < 7; ++i) {  // left layers 15-28 (the one at 22 with d = 1)
@@ -144,6 +161,19 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
     PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF1, PPNS::BUF0, 2 * i + 1 == 7 ? 1 : 2, F1, F0);
   }
   st(5);
+  // the combine's inputs (x and the parked right-head rows of this lane's output rows), fetched
+  // before the left head so that their latency hides under it
+  float xv[HO::ROWS], rv[HO::ROWS];
+#pragma unroll
+  for (int k = 0; k < HO::ROWS; ++k) {
+    const int p = tl.base + HO::row(k);
+    xv[k] = in_range(p, L) ? tl.x[p] : 0.f;
+#if RDN_HYB_PARK
+    rv[k] = (float)parked_row<MODE_H8, NBK>(tl, y, n, k, H, T);
+#else
+    rv[k] = rk[k];
+#endif
+  }
   float l[PPNS::HN];
   PPNS::head<EDGE>(t16, PPNS::BUF0, F0, F1, false, l);
   // hand the left head's rows (ping-pong lane layout) to the right head's (HeadOut) through LDS
@@ -160,11 +190,8 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, const uint8_t* blo
   const bool sat = range_vote(tl, PPNS::BUF1 + 4 * PPNS::WB, status);
   float o[HO::ROWS];
 #pragma unroll
-  for (int k = 0; k < HO::ROWS; ++k) {      // x - (r + l)/2, one rounding
-    const int p = tl.base + HO::row(k);
-    const float xv = in_range(p, L) ? tl.x[p] : 0.f;
-    o[k] = (float)((double)xv - (parked_row<MODE_H8, NBK>(tl, y, n, k, H, T) + (double)lrow[HO::row(k)]) * 0.5);
-  }
+  for (int k = 0; k < HO::ROWS; ++k)        // x - (r + l)/2, one rounding
+    o[k] = (float)((double)xv[k] - ((double)rv[k] + (double)lrow[HO::row(k)]) * 0.5);
   if (sat) nan_rows(o);
   store_out<MODE_H8, NBK>(tl, y, n, o, H, T);
   st(6);
