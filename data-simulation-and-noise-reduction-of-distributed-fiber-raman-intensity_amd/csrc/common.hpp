@@ -41,6 +41,9 @@ constexpr int CORR_SLOT = 63;
 #define RDN_F16MIX_TAIL 5
 #endif
 constexpr int F16MIX_TAIL = RDN_F16MIX_TAIL;
+// RDN_F16MIX blob records after RRCDNet's 29 big layers: 29 the left head (ping-pong head record),
+// 30 the right head as an f16 + e4m3 layer record (cout 0, copied to cout 32; inplace.hpp head_h8_mfma)
+constexpr int F16MIX_LHEAD_REC = 29, F16MIX_RHEAD_REC = 30;
 // RDN_F16MIX spiked-tile fallback: a tile whose input window holds a value outside
 // [F16MIX_WIN_LO, F16MIX_WIN_HI] runs every layer corrected (the RDN_F16F8 body on the same blob).
 // The simulator's clean signal is min-max normalised to [0, 1] and its Gaussian noise stays below

@@ -334,7 +334,11 @@ template <> struct Op<MODE_H8> {
     b.h[0] = *(const f16x8*)(act + ad[0] + off);
     b.h[1] = *(const f16x8*)(act + ad[1] + off);
     if (cin) {
+#if defined(RDN_ABLATE_NOCREAD)        // diagnostic (tools/ablate.py): no e4m3 plane reads, wrong results
+      const i32x4v ch = __builtin_bit_cast(i32x4v, b.h[0]), cl = __builtin_bit_cast(i32x4v, b.h[1]);
+#else
       const i32x4v ch = *(const i32x4v*)(act + ad[2] + off), cl = *(const i32x4v*)(act + ad[3] + off);
+#endif
       b.c = __builtin_shufflevector(ch, cl, 0, 1, 2, 3, 4, 5, 6, 7);
     }
     return b;
@@ -460,13 +464,8 @@ __device__ __forceinline__ float quarter_sum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);                   // and the other 16-lane row
 }
 
-struct NoPre {
-  __device__ void operator()() const {}
-};
-// pre(): issued right after the head's weight loads (a caller's prefetch that must not sit in front
-// of them in the vector-memory queue)
-template <int MODE, int NBK = 4, class Pre = NoPre>
-__device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[HeadOut<MODE, NBK>::ROWS], Pre pre = Pre{}) {
+template <int MODE, int NBK = 4>
+__device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[HeadOut<MODE, NBK>::ROWS]) {
   using TG = TileGeo<NBK>;
   const cfloat* hw = small_slot(tl, slot);
   if constexpr (HeadOut<MODE, NBK>::VEC) {
@@ -484,7 +483,6 @@ __device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[Hea
 #pragma unroll
       for (int i = 0; i < 16; ++i) wv[t][i] = hwv[3 * chan(4 * (i >> 3) + q, i & 7) + t];
     const float bias = hw[192];
-    pre();
     if constexpr (MODE == MODE_H8) {
       // f16 plane by v_fma_mix_f32 (the f16 operand converted inside the FMA), e4m3-lo plane into a
       // separate packed accumulator (v_pk_fma_f32 on the pairs v_cvt_pk_f32_fp8 returns), scaled by
@@ -692,7 +690,8 @@ __device__ __forceinline__ void two_sum(f32x4& hi, f32x4& c) {
 // mixed network is written as straight runs of one instantiation each (fused_inplace.hip).
 template <int MODE, int EPI, int S, bool EDGE = true, int NBK = 4, bool CIN = true, bool COUT = true,
           bool LOADC = true>
-__device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4], LayerA<MODE>& a, bool has_next) {
+__device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4], LayerA<MODE>& a, bool has_next,
+                                     const uint8_t* next_rec = nullptr) {
   using O = Op<MODE>;
   constexpr bool cin = MODE != MODE_H8 || CIN;
   constexpr bool cout = MODE != MODE_H8 || COUT;
@@ -704,7 +703,9 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   const int mp = w & 1, nq = w >> 1;
   const int q = lane >> 4, c16 = lane & 15;
   const uint8_t* wcur = tl.big + (size_t)tl.layer * LayerBytes<MODE>::BYTES;
-  const uint8_t* wnext = wcur + LayerBytes<MODE>::BYTES;
+  // the record whose operands has_next prefetches: the next layer's, or next_rec (RDN_F16MIX: the
+  // right head's record after the last corrected layer)
+  const uint8_t* wnext = next_rec ? next_rec : wcur + LayerBytes<MODE>::BYTES;
   // bf16 modes start the accumulators at the folded bias; exact fp32 keeps the reference's
   // order (sum of products, then + bias) for its 1e-5 parity
   constexpr bool BIAS_INIT = MODE != MODE_F32;
@@ -816,7 +817,13 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
       v = (EPI & RELU) ? h8_sat<true>(v) : h8_sat<false>(v);
       if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};
       if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
+#if defined(RDN_ABLATE_NOSPLIT)         // diagnostic (tools/ablate.py): no e4m3 split VALU, wrong results
+      x[mm].hi = __builtin_convertvector(v, f16x4);
+      x[mm].hi8 = __float_as_uint(v[0]);
+      x[mm].lo8 = __float_as_uint(v[1]);
+#else
       x[mm] = h8_split(v);
+#endif
     }
     const uint32_t off = (uint32_t)(BR * j + 16 * i) * ROWB_F32;
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -951,6 +958,34 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   store_block(NB - 1);
   lds_barrier();                   // the layer's output is complete
   tl.layer += 1;
+}
+
+// Conv1d(64, 1, 3) head on the MFMA for the f16 + e4m3 tile (RDN_F16MIX RRCDNet's right head): the
+// corrected layer product W.X ~= W_hi.X_hi + [W_lo | W_hi].[X_hi | X_lo] with one meaningful output
+// channel, whose record (pack.cpp pack_head_h8mfma) holds the head at couts 0 and 32, so the operands
+// a conv prefetched for M-tile 2 mp of every wave (a[0], its bias and scales) are the head's.  Rows
+// as HeadOut<MODE_H8, NBK> (N-tile 8k + w, row 128k + 16w + c16): out[k] on the lanes of quarter 0,
+// which HeadOut::writer() selects.  Replaces the VALU head (48 per-lane weight loads, 16 channels x 3
+// taps of fma_mix / e4m3-decode FMAs per row and lane, a cross-quarter sum: 12.9k cycles per tile in
+// the hybrid, tools/hyb_stamps.py) by 9 MFMAs and 12 conflict-free B reads per row block.
+template <int NBK>
+__device__ __forceinline__ void head_h8_mfma(const Tile& tl, const LayerA<MODE_H8>& a, float (&out)[NBK]) {
+  using O = Op<MODE_H8>;
+  using TG = TileGeo<NBK>;
+  const int tid = opaque_tid(), lane = tid & 63, w = tid >> 6, q = lane >> 4, c16 = lane & 15;
+  f32x4 acc[NBK];
+#pragma unroll
+  for (int k = 0; k < NBK; ++k) acc[k] = a.bias[0];
+#pragma unroll
+  for (int s = 0; s < O::KSTEPS; ++s) {
+#pragma unroll
+    for (int k = 0; k < NBK; ++k) {
+      const typename O::B b = O::load_b(tl.lds, TG::row(128 * k + 16 * w + c16 + s - 1), s, q);
+      acc[k] = O::mma(a.v[0][s], b, acc[k], a.sc[0], s);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NBK; ++k) out[k] = acc[k][0];
 }
 
 // partial sums per accumulator (S = 0: one chain with compensated chunk sums, see two_sum): F32

@@ -147,9 +147,10 @@ int big_layers(const std::vector<Op>& spec, int dtype) {
   const bool head_big = lay == BF16 || lay == F16;
   int n = 0;
   for (const Op& o : spec) n += o.kind == OpKind::BIG || (o.kind == OpKind::HEAD && head_big);
-  // RDN_F16MIX: the last head (RRCDNet's left_net.19) also as a ping-pong head record after the big
-  // layers (fused_inplace.hip rrcdnet_hybrid runs the left branch on the ping-pong engine)
-  if (dtype == F16MIX) ++n;
+  // RDN_F16MIX: the left head (left_net.19) also as a ping-pong head record after the big layers
+  // (fused_inplace.hip rrcdnet_hybrid runs the left branch on the ping-pong engine), then the right
+  // head (right_net.18) as an f16 + e4m3 layer record (its MFMA head, inplace.hpp head_h8_mfma)
+  if (dtype == F16MIX) n += 2;
   return n;
 }
 
@@ -410,6 +411,21 @@ static void pack_head_h8(const Folded& f, uint8_t* dst) {
   std::memcpy(dst + H8_BIAS_OFF, rec.data() + BIG_FRAG_BYTES_BF16, C * sizeof(float));
 }
 
+// a head (cout = 1) as an f16 + e4m3 layer record with its output channel at couts 0 and 32 (the
+// first M-tile of either output-channel half of the in-place wave pair) and zeros elsewhere
+static void pack_head_h8mfma(const Folded& f, uint8_t* dst) {
+  Folded g;
+  g.cout = C;
+  g.cin = C;
+  g.w.assign((size_t)C * C * 3, 0.0);
+  g.b.assign(C, 0.0);
+  for (int co : {0, 32}) {
+    for (int k = 0; k < C * 3; ++k) g.w[(size_t)co * C * 3 + k] = f.w[k];
+    g.b[co] = f.b[0];
+  }
+  pack_big_h8(g, dst);
+}
+
 static void pack_small_conv(const Folded& f, float* slot) {   // w[c*3+t], bias at 192 (+c)
   std::memset(slot, 0, SMALL_SLOT_FLOATS * sizeof(float));
   if (f.cin == 1) {
@@ -514,7 +530,8 @@ std::string pack(int arch, int dtype, const float* const* tensors, const int64_t
         if (!fold(rd, o, C, 1, f)) return rd.err;
         pack_small_conv(f, small + o.slot * SMALL_SLOT_FLOATS);
         if (layout == BF16 || layout == F16) pack_big_bf16(f, big + (layer++) * big_bytes, layout == F16);
-        else if (dtype == F16MIX && &o == &spec.back()) pack_head_h8(f, big + (layer++) * big_bytes);
+        else if (dtype == F16MIX && &o == &spec.back()) pack_head_h8(f, big + (size_t)F16MIX_LHEAD_REC * big_bytes);
+        else if (dtype == F16MIX) pack_head_h8mfma(f, big + (size_t)F16MIX_RHEAD_REC * big_bytes);
         break;
       case OpKind::CBAM:
         if (!pack_cbam(rd, o, small)) return rd.err;

@@ -43,21 +43,18 @@ struct H8Stage {
   }
 };
 
-#ifndef RDN_HYB_PARK
-#define RDN_HYB_PARK 0
-#endif
-
 // Diagnostic builds (tools/hyb_stamps.py, -DRDN_HYB_STAMPS=1): s_memtime at the phase boundaries of
 // the hybrid body, summed over workgroups into the range workspace behind its status word (u64
-// [1 + phase], [9] = workgroups).  In the product build every stamp compiles to nothing.
+// [1 + phase], [1 + HYB_PHASES] = workgroups).  In the product build every stamp compiles to nothing.
 #ifndef RDN_HYB_STAMPS
 #define RDN_HYB_STAMPS 0
 #endif
+constexpr int HYB_PHASES = 10;
 struct HybStamps {
-  unsigned long long t, acc[8];
+  unsigned long long t, acc[HYB_PHASES];
   __device__ __forceinline__ HybStamps() {
     if (RDN_HYB_STAMPS) {
-      for (int k = 0; k < 8; ++k) acc[k] = 0;
+      for (int k = 0; k < HYB_PHASES; ++k) acc[k] = 0;
       t = __builtin_amdgcn_s_memtime();
     }
   }
@@ -71,8 +68,8 @@ struct HybStamps {
   __device__ __forceinline__ void flush(unsigned* status) {
     if (RDN_HYB_STAMPS && status && __builtin_amdgcn_workitem_id_x() == 0) {
       unsigned long long* w = (unsigned long long*)status;
-      for (int k = 0; k < 8; ++k) atomicAdd(w + 1 + k, acc[k]);
-      atomicAdd(w + 9, 1ull);
+      for (int k = 0; k < HYB_PHASES; ++k) atomicAdd(w + 1 + k, acc[k]);
+      atomicAdd(w + 1 + HYB_PHASES, 1ull);
     }
   }
 };
@@ -97,6 +94,7 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, float* y, int n, i
     // the stem tests its inputs against the window; one word per wave at the end of the LDS (first
     // written by layer 0, after the barrier below and the read behind it)
     const bool out = PPNS::stem(t16, 0, PPNS::BUF0, xr, F16MIX_WIN_LO, F16MIX_WIN_HI);
+    st(0);
     unsigned* vote = (unsigned*)(tl.lds + PPNS::LDS_BYTES) - PPNS::WAVES;
     const bool wave_out = __builtin_amdgcn_ballot_w64(out) != 0;
     if ((PPNS::tid() & 63) == 0) vote[PPNS::tid() >> 6] = wave_out ? 1u : 0u;
@@ -109,7 +107,7 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, float* y, int n, i
     __syncthreads();
     if (spiked) return false;
   }
-  st(0);
+  st(1);
   f32x4 id[16 * NBK / 4];
   LayerA<MODE_H8> a;
   // layers 0 .. PP - 1 plain, layer PP (the tail's producer) staged into the in-place planes
@@ -117,6 +115,7 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, float* y, int n, i
     PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1);
     PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF1, PPNS::BUF0, 1, F1, F0);
   }
+  st(2);
   {
     H8Stage stg;
     if constexpr (PP % 2 == 1) {
@@ -131,36 +130,35 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, float* y, int n, i
   tl.layer = PP + 1;
   load_layer_a<MODE_H8>(tl, PP + 1, a);
   __syncthreads();
-  st(1);
-  for (int i = 0; i < TAIL; ++i) conv<MODE_H8, RELU, 1, EDGE, NBK, true, true, true>(tl, 1, id, a, i + 1 < TAIL);
-  st(2);
-  // the left stem's inputs, issued right behind the head's weight loads (not before them: a wait for
-  // the weights would wait for these too), so their latency hides under the head (the left stem
-  // waited on them: 6.2k cycles per tile, tools/hyb_stamps.py)
-  PPNS::StemX xl;
-  double r[HO::ROWS];
-  head<MODE_H8, NBK>(tl, 2, r, [&] { xl = PPNS::stem_load(t16); });
-#if RDN_HYB_PARK
-  park_rows<MODE_H8, NBK>(tl, y, n, r, H, T);
-#else
-  float rk[HO::ROWS];            // the right head's rows, rounded as parking them in y would
-  round_rows(r, rk);
-#endif
+  st(3);
+  // the last corrected layer prefetches the right head's record (its operands: a[0])
+  const uint8_t* rhead = tl.big + (size_t)F16MIX_RHEAD_REC * BIG_BYTES_H8;
+  for (int i = 0; i < TAIL; ++i)
+    conv<MODE_H8, RELU, 1, EDGE, NBK, true, true, true>(tl, 1, id, a, true, i + 1 < TAIL ? nullptr : rhead);
+  st(4);
+  // the left stem's inputs, fetched now: their latency hides under the right head (whose operands
+  // are in registers already: no vector-memory wait in it)
+  const PPNS::StemX xl = PPNS::stem_load(t16);
+  float rk[HO::ROWS];            // the right head's rows, kept over the left branch
+  head_h8_mfma<NBK>(tl, a, rk);
+  st(5);
   // left branch: layers 15-28 and the head on the ping-pong engine (f16 activations into the head,
   // whose weights carry their rounding residue: tools/head_fusion_emul.py puts this at 1.52e-2 on
   // trained RRCDNet against 1.44e-2 with the split head, the bar being 2e-2)
   t16.layer = 15;
   PPNS::load_frags(t16, 15, F0);
-  __syncthreads();               // the left stem overwrites the rows the right head just read
-  st(3);
+  // the left stem overwrites the rows the right head just read: an LDS-only barrier (a __syncthreads
+  // would also wait for the vector-memory loads in flight: the left stem's x and F0)
+  PPNS::lds_barrier();
+  st(6);
   PPNS::stem(t16, 1, PPNS::BUF0, xl);
   PPNS::lds_barrier();
-  st(4);
+  st(7);
   for (int i = 0; i < 7; ++i) {  // left layers 15-28 (the one at 22 with d = 1)
     PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 2, F0, F1);
     PPNS::layer<PPNS::RELU, EDGE>(t16, PPNS::BUF1, PPNS::BUF0, 2 * i + 1 == 7 ? 1 : 2, F1, F0);
   }
-  st(5);
+  st(8);
   // the combine's inputs (x and the parked right-head rows of this lane's output rows), fetched
   // before the left head so that their latency hides under it
   float xv[HO::ROWS], rv[HO::ROWS];
@@ -168,11 +166,7 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, float* y, int n, i
   for (int k = 0; k < HO::ROWS; ++k) {
     const int p = tl.base + HO::row(k);
     xv[k] = in_range(p, L) ? tl.x[p] : 0.f;
-#if RDN_HYB_PARK
-    rv[k] = (float)parked_row<MODE_H8, NBK>(tl, y, n, k, H, T);
-#else
     rv[k] = rk[k];
-#endif
   }
   float l[PPNS::HN];
   PPNS::head<EDGE>(t16, PPNS::BUF0, F0, F1, false, l);
@@ -194,7 +188,7 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, float* y, int n, i
     o[k] = (float)((double)xv[k] - ((double)rv[k] + (double)lrow[HO::row(k)]) * 0.5);
   if (sat) nan_rows(o);
   store_out<MODE_H8, NBK>(tl, y, n, o, H, T);
-  st(6);
+  st(9);
   st.flush(status);
   return true;
 }

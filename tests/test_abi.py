@@ -335,16 +335,33 @@ def test_pack_layout_f16mix_head_record():
     """RDN_F16MIX blob: the 29 f16 + e4m3 big layers, then the left head (left_net.19) as a ping-pong head
     record in an f16 + e4m3-sized slot: f16 fragments with cout 0 in rows 0 and 32 (M-tiles 0 and 2)
     and its weights' f16 rounding residue in rows 1 and 33, the bias at H8_BIAS_OFF (fused16.hpp head,
-    read by fused_inplace.hip rrcdnet_hybrid)."""
+    read by fused_inplace.hip rrcdnet_hybrid); then the right head (right_net.18) as an f16 + e4m3 layer
+    record with the head at couts 0 and 32 (inplace.hpp head_h8_mfma)."""
     from raman_mi355x import engine
     sd = golden_state_dict("RRCDNet", "trained")
     blob = engine.pack("RRCDNet", sd, "f16mix", "cpu").numpy()
-    assert blob.size == engine.packed_size("RRCDNet", "f16mix") == SMALL + 30 * 50432
+    assert blob.size == engine.packed_size("RRCDNet", "f16mix") == SMALL + 31 * 50432
     # the big layers are the f16f8 blob's
     ref = engine.pack("RRCDNet", sd, "f16f8", "cpu").numpy()
     np.testing.assert_array_equal(blob[SMALL:SMALL + 29 * 50432], ref[SMALL:])
+    lane = np.arange(64)
+    # the right head's record: f16 fragments of cout 0 in rows 0 and 32, zeros elsewhere, bias copied
+    wr, br = _fold(sd, "right_net.18", None)
+    R2 = blob[SMALL + 30 * 50432:]
+    main = R2[:24576].view(np.float16).reshape(4, 6, 64, 8)
+    for s_ in range(6):
+        t, u = s_ >> 1, s_ & 1
+        for j in range(8):
+            cin = 32 * u + 4 * (lane >> 4) + (j & 3) + 16 * (j >> 2)
+            for m in (0, 2):
+                got = main[m, s_, :, j]
+                np.testing.assert_array_equal(got[(lane & 15) == 0], wr[0, cin, t][(lane & 15) == 0].astype(np.float16))
+                assert np.all(got[(lane & 15) != 0] == 0)
+        assert np.all(main[1, s_] == 0) and np.all(main[3, s_] == 0)
+    rbias = R2[50176:].view(np.float32)
+    assert rbias[0] == np.float32(br[0]) and rbias[32] == np.float32(br[0]) and np.count_nonzero(rbias) <= 2
     w, b = _fold(sd, "left_net.19", None)            # [1, 64, 3]
-    R = blob[SMALL + 29 * 50432:]
+    R = blob[SMALL + 29 * 50432:SMALL + 30 * 50432]
     frag = R[:24576].view(np.float16).reshape(4, 6, 64, 8)
     lane = np.arange(64)
     for s_ in range(6):

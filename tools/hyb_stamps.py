@@ -13,9 +13,10 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fiber-raman-intensity_amd"))
-PHASES = ["right stem + window vote", "right ping-pong layers 0-9 (9 staged)", "in-place corrected tail (5)",
-          "right head + park", "left stem", "left layers 15-28 (14)", "left head + vote + combine + store"]
-PER_LAYER = {1: 10, 2: 5, 5: 14}
+PHASES = ["right stem", "window vote", "right ping-pong layers 0-7", "layers 8, 9 (staged) + tail operands",
+          "in-place corrected tail (5)", "right head (MFMA)", "left layer-0 operands + barrier", "left stem",
+          "left layers 15-28 (14)", "left head + vote + combine + store"]
+PER_LAYER = {2: 8, 4: 5, 8: 14}
 
 
 def main():
@@ -54,8 +55,8 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     w = ws.view(torch.int64).cpu().tolist()
-    n = w[9]
-    tot = sum(w[1:8])
+    n = w[1 + len(PHASES)]
+    tot = sum(w[1:1 + len(PHASES)])
     print(f"{e0.elapsed_time(e1) / 5:.2f} ms per forward of {B} spectra; {n} hybrid workgroups stamped; "
           f"{tot / n:.0f} cycles per workgroup")
     for k, name in enumerate(PHASES):
