@@ -91,20 +91,15 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, float* y, int n, i
   PPNS::load_frags(t16, 0, F0);
   const PPNS::StemX xr = PPNS::stem_load(t16);
   {
-    // the stem tests its inputs against the window; one word per wave at the end of the LDS (first
-    // written by layer 0, after the barrier below and the read behind it)
+    // the stem tests its inputs against the window.  Every wave reads the x of ALL the tile's rows
+    // (wave w computes channel slot w of rows lane + 64k), so each wave's ballot is already the
+    // tile's vote: no LDS vote words and no second barrier (2.5k cycles per tile, tools/hyb_stamps.py)
     const bool out = PPNS::stem(t16, 0, PPNS::BUF0, xr, F16MIX_WIN_LO, F16MIX_WIN_HI);
     st(0);
-    unsigned* vote = (unsigned*)(tl.lds + PPNS::LDS_BYTES) - PPNS::WAVES;
-    const bool wave_out = __builtin_amdgcn_ballot_w64(out) != 0;
-    if ((PPNS::tid() & 63) == 0) vote[PPNS::tid() >> 6] = wave_out ? 1u : 0u;
+    const bool spiked = __builtin_amdgcn_ballot_w64(out) != 0;
+    // the stem's rows are complete before layer 0 reads them; on a spiked tile, before the fallback
+    // body overwrites the LDS
     PPNS::lds_barrier();
-    bool spiked = false;
-#pragma unroll
-    for (int k = 0; k < PPNS::WAVES; ++k) spiked = spiked || vote[k] != 0;
-    // every wave has read the votes before any wave writes again: the fallback body's stem, or layer
-    // 0's epilogue, whose last rows are the vote words
-    __syncthreads();
     if (spiked) return false;
   }
   st(1);
@@ -124,12 +119,15 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, float* y, int n, i
     } else {
       PPNS::layer<PPNS::STAGE, EDGE>(t16, PPNS::BUF0, PPNS::BUF1, 1, F0, F1, false, nullptr, nullptr, &stg);
     }
+    // the tail's operands, issued before the staged planes are written so that their latency hides
+    // under the stores; then an LDS-only barrier (the first conv waits for its k-step's operands
+    // alone, not for all 96 VGPRs of them as a __syncthreads would)
+    load_layer_a<MODE_H8>(tl, PP + 1, a);
     stg.write<EDGE>(tl.lds, t16);
     tl.amax = fmaxf(tl.amax, stg.amax);
   }
   tl.layer = PP + 1;
-  load_layer_a<MODE_H8>(tl, PP + 1, a);
-  __syncthreads();
+  lds_barrier();
   st(3);
   // the last corrected layer prefetches the right head's record (its operands: a[0])
   const uint8_t* rhead = tl.big + (size_t)F16MIX_RHEAD_REC * BIG_BYTES_H8;

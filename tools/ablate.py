@@ -24,7 +24,7 @@ VARIANTS = {"base": "", "prev": "", "cur": "", "cur2": "", "nolds": "-DRDN_ABLAT
             "tail0": "-DRDN_F16MIX_TAIL=0", "tail2": "-DRDN_F16MIX_TAIL=2", "hybstamps": "-DRDN_HYB_STAMPS=1",
             "touch0": "-DRDN_HYB_TOUCH_AHEAD=0", "touch512": "-DRDN_HYB_TOUCH_AHEAD=512",
             "f6": "-DRDN_ABLATE_F6", "nocread": "-DRDN_ABLATE_NOCREAD", "nosplit": "-DRDN_ABLATE_NOSPLIT",
-            "mhead": "", "lbar": ""}
+            "mhead": "", "lbar": "", "stg": "", "vote": ""}
 
 
 def build():
