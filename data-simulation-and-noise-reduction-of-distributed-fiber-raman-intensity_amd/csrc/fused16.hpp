@@ -379,7 +379,7 @@ __device__ __forceinline__ void zero_outside(const Tile& tl, uint32_t dst, int r
 }
 
 struct NoStage {
-  __device__ void put(int, f32x8) {}
+  __device__ void put(int, f32x8, bool) {}
 };
 template <int EPI, bool EDGE, class SG = NoStage>
 __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int dil, const Frags& F, Frags& G,
@@ -436,7 +436,10 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     // pay the per-lane check and select; the other N-tiles of an edge tile store unmasked
     constexpr bool valid = true;             // rows outside [0, L): zero_outside after the loop
     if constexpr (EPI == STAGE) {
-      stg->put(n, __builtin_shufflevector(a.v[0], a.v[1], 0, 1, 2, 3, 4, 5, 6, 7));
+      // valid: the row's position lies in [0, L) (only there may the range guard see the value: the
+      // rows of an edge tile beyond L + 1 are computed from rows no wave keeps current)
+      stg->put(n, __builtin_shufflevector(a.v[0], a.v[1], 0, 1, 2, 3, 4, 5, 6, 7),
+               !EDGE || in_range(pos0 + NR * n + (lane & 15), tl.L));
       return;
     }
     V* p = (V*)(tl.lds + sa + n * NR * ROWB);

@@ -258,25 +258,6 @@ __device__ __forceinline__ bool window_outside(const Tile& tl, float lo, float h
   return any;
 }
 
-// Touches (one load per 128-B line) the x rows of the tile that will most likely run next on this
-// CU -- workgroup id + CUs, dispatched to the same XCD once the current wave of tiles drains -- so
-// its stem finds them in L2 instead of waiting on HBM.  Issued together with this tile's own stem
-// loads (which wait on HBM anyway: an older load in flight delays every younger one's wait); the
-// value is consumed by nothing.
-#ifndef RDN_HYB_TOUCH_AHEAD
-#define RDN_HYB_TOUCH_AHEAD 256   // MI355X's CUs (0: off)
-#endif
-__device__ __forceinline__ void touch_next_x(const float* x, int L, int T, int tiles, int64_t id, int64_t total) {
-  constexpr int LINES = (TileGeo<5>::WB + 2 + 31) / 32 + 1;
-  const int lane = __builtin_amdgcn_workitem_id_x();
-  const int64_t nid = id + RDN_HYB_TOUCH_AHEAD;
-  if (nid >= total || lane >= LINES) return;
-  const int n = (int)(nid / tiles), base = (int)(nid - (int64_t)n * tiles) * T - fused_halo(RRCDNET);
-  const int p = base - 1 + 32 * lane;
-  const float v = x[(size_t)n * L + (p < 0 ? 0 : p < L ? p : L - 1)];
-  asm volatile("" ::"v"(v));
-}
-
 // RDN_F16MIX RRCDNet: hybrid bodies on 640-row tiles, the in-place body on short last tiles; a tile
 // whose input window leaves [F16MIX_WIN_LO, F16MIX_WIN_HI] (a spike) runs every layer corrected
 template <int TAIL>
@@ -287,8 +268,6 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restr
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
   if (!f16mix_blob_ok(blob)) return nan_outputs(tl, y, n, T);
-  if (RDN_HYB_TOUCH_AHEAD > 0)
-    touch_next_x(x, L, T, tiles, __builtin_amdgcn_workgroup_id_x(), (int64_t)__builtin_amdgcn_grid_size_x() / THREADS);
   const int need = L - tl.base + 2;
   if (tl.base >= 0 && tl.base + TileGeo<5>::WB <= L) {
     if (!hyb640::rrcdnet_hybrid_body<false, TAIL>(tl, y, n, L, T, status))

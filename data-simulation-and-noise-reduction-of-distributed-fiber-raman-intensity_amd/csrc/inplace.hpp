@@ -813,9 +813,9 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
     for (int mm = 0; mm < MT; ++mm) {
       f32x4 v = res[j][i][mm];
       if (EPI & ADD_ID) v += id[(j * NT + i) * MT + mm];
+      if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};      // the range guard sees rows in [0, L) only
       h8_track<(EPI & RELU) != 0>(tl.amax, v);
       v = (EPI & RELU) ? h8_sat<true>(v) : h8_sat<false>(v);
-      if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};
       if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
 #if defined(RDN_ABLATE_NOSPLIT)         // diagnostic (tools/ablate.py): no e4m3 split VALU, wrong results
       x[mm].hi = __builtin_convertvector(v, f16x4);
@@ -1044,6 +1044,23 @@ __device__ __forceinline__ bool range_vote(const Tile& tl, uint32_t vote_off, un
   for (int k = 0; k < THREADS / 64; ++k) sat = sat || vote[k] != 0;
   __syncthreads();
   if (sat && status && tid == 0) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return sat;
+}
+// The same vote split around a caller's barrier (the RDN_F16MIX hybrid publishes it with its own
+// LDS hand-off, one barrier instead of three): post this wave's word, then -- after a barrier, with
+// nothing writing the words again in the tile -- read every wave's
+__device__ __forceinline__ void range_vote_post(const Tile& tl, uint32_t vote_off) {
+  const int tid = __builtin_amdgcn_workitem_id_x();
+  const bool wave_sat = __builtin_amdgcn_ballot_w64(tl.amax > H8_SAT) != 0;
+  if ((tid & 63) == 0) ((unsigned*)(tl.lds + vote_off))[tid >> 6] = wave_sat ? 1u : 0u;
+}
+__device__ __forceinline__ bool range_vote_read(const Tile& tl, uint32_t vote_off, unsigned* status) {
+  const unsigned* vote = (const unsigned*)(tl.lds + vote_off);
+  bool sat = false;
+#pragma unroll
+  for (int k = 0; k < THREADS / 64; ++k) sat = sat || vote[k] != 0;
+  if (sat && status && __builtin_amdgcn_workitem_id_x() == 0)
+    __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return sat;
 }
 template <int N>

@@ -14,9 +14,13 @@ struct H8Stage {
   f16x8 hi[PPNS::NT];
   uint32_t e_hi[PPNS::NT][2], e_lo[PPNS::NT][2];
   float amax = 0.f;              // range guard (inplace.hpp h8_track): merged into the tile's after the layer
-  __device__ __forceinline__ void put(int n, PPNS::f32x8 v) {
-    h8_track<true>(amax, __builtin_shufflevector(v, v, 0, 1, 2, 3));
-    h8_track<true>(amax, __builtin_shufflevector(v, v, 4, 5, 6, 7));
+  // valid: the row lies in [0, L); rows outside are written as zeros (write) and never tracked -- on
+  // an edge tile the rows beyond L + 1 are computed from stale LDS rows (the ping-pong engine's idle
+  // waves skip them), whose values are arbitrary and would raise a false range error
+  __device__ __forceinline__ void put(int n, PPNS::f32x8 v, bool valid) {
+    const PPNS::f32x8 t = valid ? v : (PPNS::f32x8)(0.f);
+    h8_track<true>(amax, __builtin_shufflevector(t, t, 0, 1, 2, 3));
+    h8_track<true>(amax, __builtin_shufflevector(t, t, 4, 5, 6, 7));
     const f32x4 a = h8_sat<true>(__builtin_shufflevector(v, v, 0, 1, 2, 3));
     const f32x4 b = h8_sat<true>(__builtin_shufflevector(v, v, 4, 5, 6, 7));
     const H8Split sa = h8_split(a), sb = h8_split(b);
@@ -169,7 +173,8 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, float* y, int n, i
   float l[PPNS::HN];
   PPNS::head<EDGE>(t16, PPNS::BUF0, F0, F1, false, l);
   // hand the left head's rows (ping-pong lane layout) to the right head's (HeadOut) through LDS
-  // (BUF1: no longer read), then y = x - (r + l)/2 with r from its parking place in y
+  // (BUF1: no longer read since layer 28's closing barrier), then y = x - (r + l)/2; the corrected
+  // tail's range vote (one word per wave behind the rows) rides on the same barrier
   float* lrow = (float*)(tl.lds + PPNS::BUF1);
   if ((PPNS::tid() & 63) < PPNS::HEAD_LANES) {
 #pragma unroll
@@ -178,8 +183,9 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, float* y, int n, i
       if (j < PPNS::WB) lrow[j] = l[k];
     }
   }
-  // the range vote of the corrected tail (its barriers also publish lrow); vote words behind lrow
-  const bool sat = range_vote(tl, PPNS::BUF1 + 4 * PPNS::WB, status);
+  range_vote_post(tl, PPNS::BUF1 + 4 * PPNS::WB);
+  PPNS::lds_barrier();
+  const bool sat = range_vote_read(tl, PPNS::BUF1 + 4 * PPNS::WB, status);
   float o[HO::ROWS];
 #pragma unroll
   for (int k = 0; k < HO::ROWS; ++k)        // x - (r + l)/2, one rounding

@@ -18,6 +18,16 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: longer CPU test")
 
 
+def pytest_collection_modifyitems(config, items):
+    """Outside the range tests, a 16-bit module forward that re-runs its batch in fp32 (input gate or
+    RDN_ERANGE) is a failure: normalised spectra never leave the 16-bit range, so the warning would
+    mean a false range detection silently hidden by the fp32 result (round 4: the 256-row hybrid's
+    edge tiles tracked rows outside [0, L))."""
+    for item in items:
+        if item.get_closest_marker("gpu") and os.path.basename(str(item.fspath)) != "test_range_gpu.py":
+            item.add_marker(pytest.mark.filterwarnings("error:.*ran in fp32 instead:RuntimeWarning"))
+
+
 def load_golden(arch):
     return np.load(os.path.join(GOLDEN, f"model_{arch}.npz"))
 

@@ -132,3 +132,35 @@ def test_module_reruns_saturated_batch_in_fp32(inputs):
     assert torch.equal(y, y32)
     y1 = m(torch.from_numpy(inputs["main_noisy"][:2]).unsqueeze(1).cuda())      # back in range: 'f16'
     assert torch.isfinite(y1).all()
+
+
+@pytest.mark.parametrize("short", ["1", "0"])
+@pytest.mark.parametrize("dtype", ["f16", "f16f8"])
+def test_no_false_range_error_after_saturated_launch(dtype, short, inputs, monkeypatch):
+    """The range guard sees only rows inside [0, L).  On an edge tile of the 256-row hybrid the rows
+    beyond L + 1 are computed from LDS rows no wave keeps current (idle waves skip them), i.e. from
+    whatever an earlier workgroup left there: a saturating launch (inputs x1000) first fills the LDS
+    with large values, then normal spectra of ragged lengths -- edge tiles with idle waves -- must run
+    without RDN_ERANGE and without NaN, in both tile geometries (RDN_SHORT_TILES)."""
+    import raman_mi355x as R
+    from raman_mi355x import engine
+    monkeypatch.setenv("RDN_SHORT_TILES", short)
+    sd = golden_state_dict("RRCDNet", "trained")
+    m = R.RRCDNet()
+    m.load_state_dict(sd, strict=True)
+    m = m.cuda().eval().set_engine_dtype(dtype)
+    code = m.engine_code
+    packed = m.packed_weights(torch.device("cuda"))
+    base = inputs["main_noisy"][:2]
+    big = torch.from_numpy((base * 1000.0).astype(np.float32)).unsqueeze(1).cuda()
+    for L in (1200, 2049, 1000, 5000, 333, 4099):
+        ws_big = engine.Workspace("RRCDNet", code, big.shape[0], big.shape[-1], big.device)
+        engine.forward("RRCDNet", code, packed, big, check=False, workspace=ws_big)
+        with pytest.raises(Exception):
+            ws_big.check()                                       # x1000 saturates (test above)
+        for B in (2, 16):
+            x = torch.from_numpy(np.ascontiguousarray(np.tile(base[:, :L], (B // 2, 1)))).unsqueeze(1).cuda()
+            ws = engine.Workspace("RRCDNet", code, B, L, x.device)
+            y = engine.forward("RRCDNet", code, packed, x, check=False, workspace=ws)
+            ws.check()                                           # no RangeError
+            assert torch.isfinite(y).all(), (dtype, short, L, B)

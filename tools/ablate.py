@@ -22,9 +22,8 @@ VARIANTS = {"base": "", "prev": "", "cur": "", "cur2": "", "nolds": "-DRDN_ABLAT
             "h16f16": "-DRDN_H16_F16=1", "h8plain": "-DRDN_ABLATE_H8_PLAIN", "nohead": "-DRDN_ABLATE_NOHEAD", "ld2": "-DRDN_H16_LDSTEP=2", "ld4": "-DRDN_H16_LDSTEP=4", "pf2": "-DRDN_H16_PF=2", "pf4": "-DRDN_H16_PF=4", "alledge": "-DRDN_ABLATE_ALLEDGE -DRDN_TEAM_STAMPS=1",
             "tail3": "-DRDN_F16MIX_TAIL=3", "tail4": "-DRDN_F16MIX_TAIL=4", "tail5": "-DRDN_F16MIX_TAIL=5", "nowin": "-DRDN_F16MIX_WIN=0", "nostem": "-DRDN_ABLATE_NOSTEM", "noheadv": "-DRDN_ABLATE_NOHEADV",
             "tail0": "-DRDN_F16MIX_TAIL=0", "tail2": "-DRDN_F16MIX_TAIL=2", "hybstamps": "-DRDN_HYB_STAMPS=1",
-            "touch0": "-DRDN_HYB_TOUCH_AHEAD=0", "touch512": "-DRDN_HYB_TOUCH_AHEAD=512",
             "f6": "-DRDN_ABLATE_F6", "nocread": "-DRDN_ABLATE_NOCREAD", "nosplit": "-DRDN_ABLATE_NOSPLIT",
-            "mhead": "", "lbar": "", "stg": "", "vote": ""}
+            "mhead": "", "lbar": "", "stg": "", "vote": "", "comb": "", "track": ""}
 
 
 def build():
