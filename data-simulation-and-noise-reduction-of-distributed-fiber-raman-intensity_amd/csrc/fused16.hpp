@@ -392,11 +392,14 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   const int pos0 = tl.base + (w % RB) * RW;
 
   // Idle waves of a short last tile: every row of this wave lies at position >= L + 2, beyond the
-  // reach (d <= 2) of any row that matters, so it skips the layer (its dst rows are never read by
-  // a stored output: positions L, L + 1 are re-zeroed by the wave that owns them, and the wrapped
-  // taps of rows 0, 1 erode into the halo like any other edge).  Its SIMD partner wave then has the
-  // MFMA pipe to itself.  It still fetches the next layer's operands and meets the barrier.
+  // reach (d <= 2) of any row that matters, so it skips the layer's MFMAs and only zeroes its dst
+  // rows.  Left unwritten they would hold whatever an earlier workgroup left in the LDS, and the
+  // wrapped taps of rows 0, 1 read them: that stays in the halo, but it made the halo rows of the
+  // 256-row hybrid arbitrarily large, which the range guard of its staged layer and corrected tail
+  // then saw (a false RDN_ERANGE after a saturating launch on the same CUs).  Its SIMD partner wave
+  // has the MFMA pipe to itself; it still fetches the next layer's operands and meets the barrier.
   if (EDGE && pos0 >= tl.L + 2) {
+    if constexpr (EPI != STAGE) zero_outside(tl, dst, pos0 - tl.base, h, lane);
     if (has_next) load_frags(tl, next, G);
     if constexpr (EPI == LINEAR_SAVE) {
 #pragma unroll

@@ -213,6 +213,18 @@ class Workspace:
                                                  ctypes.c_void_p(self.stream.cuda_stream)), "rdn_workspace_size")
         return sz.value
 
+    def range_word(self):
+        """The range word of a fused network's RDN_F16F8 / RDN_F16MIX workspace (its first 4 bytes,
+        rdn_forward_status's word) as a device int32 tensor, without waiting: one element of a
+        caller's single device-to-host read (models._EngineNet.forward).  A caller that reads it
+        this way clears it with clear_range_word() (rdn_forward_status reads and clears)."""
+        if self.arch in CBAM_IDS or self.code not in RANGE_CODES:
+            raise ValueError("range_word: only the fused networks' range-checked workspaces")
+        return self.buf[:4].view(torch.int32)
+
+    def clear_range_word(self):
+        self.buf[:4].zero_()
+
     def check(self):
         """Wait for the stream; raise if a CBAM hand-off of any forward since the last check timed out."""
         _lib.check(_lib.lib().rdn_forward_status(self.arch, self.code, self.n, self.L, self.ptr, self.bytes,

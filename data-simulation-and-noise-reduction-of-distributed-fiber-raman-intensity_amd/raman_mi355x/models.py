@@ -50,11 +50,6 @@ C = 64
 INPUT_GATE = 4.0
 
 
-def _absmax(x):
-    lo, hi = torch.aminmax(x)                     # one pass, no |x| copy; syncs the stream
-    return max(-float(lo), float(hi))
-
-
 def _conv(cin=C, cout=C, dilation=1, bias=True, k=3):
     return nn.Conv1d(cin, cout, k, padding=dilation * (k // 2), dilation=dilation, bias=bias)
 
@@ -182,13 +177,25 @@ class _EngineNet(nn.Module):
             raise TypeError(f"{type(self).__name__}: expected float32 input, got {x.dtype}")
         code = self._engine_code
         why = None
+        ws = self._workspace(x)
         try:
-            y = engine.forward(self.ARCH, code, self.packed_weights(x.device), x, workspace=self._workspace(x))
+            # a fused network's range word is read below together with the input gate (one wait per
+            # call); the CBAM networks check their own workspace inside engine.forward
+            y = engine.forward(self.ARCH, code, self.packed_weights(x.device), x, check=ws is None, workspace=ws)
         except _lib.RangeError:
             # an activation left the e4m3 planes' range: never return the NaN tiles
             why = "activations beyond the e4m3 planes' range (|v| > 1792)"
-        if why is None and code != 0 and x.numel() and _absmax(x) > INPUT_GATE:
-            why = f"|input| beyond {INPUT_GATE} (outside normalised intensity)"
+        if why is None and code != 0 and x.numel():
+            lo, hi = torch.aminmax(x)                         # one pass, no |x| copy
+            parts = [lo.reshape(1), hi.reshape(1)]
+            if ws is not None:
+                parts.append(ws.range_word().to(torch.float32))
+            h = torch.cat(parts).tolist()                      # the call's one host wait
+            if ws is not None and h[2] != 0:
+                ws.clear_range_word()
+                why = "activations beyond the e4m3 planes' range (|v| > 1792)"
+            elif max(-h[0], h[1]) > INPUT_GATE:
+                why = f"|input| beyond {INPUT_GATE} (outside normalised intensity)"
         if why is None:
             return y
         # the batch is re-run in exact fp32, which has neither bound
