@@ -308,7 +308,7 @@ __global__ __launch_bounds__(THREADS) void segment(const uint8_t* __restrict__ b
 // atomic add by lane 0; lane 0 polls the counter with sc1 loads, a workgroup barrier, then sc1 loads
 // of the slots.  The ResidualBlock identity (the block input, all tile rows) is parked in a
 // per-workgroup fp32 buffer in memory (sc1 stores / loads: written and read back by the same CU).
-// A wait that exceeds SPIN_LIMIT polls raises the error word and falls through instead of hanging.
+// A wait that exceeds SPIN_TICKS (0.3 s) raises the error word and falls through instead of hanging.
 
 // Halo exchange: the tiles of a team meet at every CBAM anyway, so instead of recomputing the whole
 // network's halo (85 / 77 rows per side for ADSDN / APIDN: 30 / 28 tiles per spectrum at L = 10,000)
@@ -323,7 +323,12 @@ constexpr int EDGE_BYTES = EDGE_ROWS * 64 * 4;       // one edge, fp32
 constexpr int STAT_BYTES = 64 * 8 + 64 * 4;        // per-tile stats: 64 fp64 sums, 64 ordered u32 maxima
 constexpr int SLOT_BYTES = STAT_BYTES + 2 * EDGE_BYTES;   // + the tile's first / last EDGE_ROWS own-edge rows
 static_assert(2 * TEAM_HALO - EDGE_ROWS >= TEAM_HALO - 1 && TEAM_HALO >= 4, "edge rows lie in the tile's own rows");
-constexpr unsigned SPIN_LIMIT = 1u << 22;          // ~0.3 s of s_sleep polls
+// A wait is bounded by wall-clock time: SPIN_TICKS of the 100 MHz s_memrealtime counter (0.3 s),
+// checked every 64 polls by one thread, which raises the error words; SPIN_LIMIT polls remain as a
+// backstop (a poll round of the tagged hand-off is a memory round trip plus a workgroup vote, so a
+// count alone stood for seconds, not the 0.3 s its comment promised: ADVICE r03).
+constexpr unsigned long long SPIN_TICKS = 30000000ull;
+constexpr unsigned SPIN_LIMIT = 1u << 22;
 #ifndef RDN_TEAM_SLEEP
 #define RDN_TEAM_SLEEP 2                           // s_sleep units (64 clocks) between two polls
 #endif
@@ -547,18 +552,19 @@ __device__ __forceinline__ void publish_stats(const Tile& tl, const TeamArgs& ta
 }
 
 // the team has arrived at `target`: lane 0 polls (sc1), the workgroup barrier releases the rest.
-// A wait that exceeds SPIN_LIMIT polls (a team member never arrived: the co-residency the grid is
+// A wait that exceeds SPIN_TICKS (a team member never arrived: the co-residency the grid is
 // sized for was broken, e.g. by a concurrent kernel) raises the error word and falls through; once
 // the word is up every later wait of every workgroup falls through at once, so the grid drains in
-// about one SPIN_LIMIT, the outputs of the affected spectra are NaN (team_forward) and the host
+// about one SPIN_TICKS, the outputs of the affected spectra are NaN (team_forward) and the host
 // reports RDN_EHIP (cbam_status).
 __device__ __forceinline__ void team_wait(const TeamArgs& ta, unsigned* ctr, unsigned target) {
   if (__builtin_amdgcn_workitem_id_x() == 0) {
     unsigned it = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(RDN_TEAM_SLEEP);
       if ((++it & 63) == 0 && __hip_atomic_load(ta.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-      if (it > SPIN_LIMIT) {
+      if (it > SPIN_LIMIT || ((it & 63) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS)) {
         __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(ta.err + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sticky word
         break;
@@ -1105,6 +1111,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
     unsigned mp = 0;
     bool failed = false, off_xcd = false;
     unsigned vparity = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (int b = 0; b < nbatch; ++b) {
       u32x2 sv[PER], mv[PER];
       bool ok[PER];
@@ -1150,7 +1157,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
           mine = mine && edge_ok;
         }
         if (wg_all(lds, mine, vparity)) break;
-        // a wait that exceeds SPIN_LIMIT rounds (a team member never published: co-residency
+        // a wait that exceeds SPIN_LIMIT rounds or SPIN_TICKS (a team member never published: co-residency
         // broken) raises the error words; once they are up every wait falls through (NaN outputs)
         if (failed || it > SPIN_LIMIT) {
           if (tid == 0 && !failed) {
@@ -1159,6 +1166,12 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
           }
           failed = true;
           break;
+        }
+        // every 64 rounds: thread 0 raises the error words once the wait passed SPIN_TICKS, and the
+        // workgroup reads them in one vote (thread 0 sees its own store: the break is uniform)
+        if ((it & 63) == 63 && tid == 0 && __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) {
+          __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(ta.err + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if ((it & 63) == 63 &&
             !wg_all(lds, __hip_atomic_load(ta.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0, vparity)) {

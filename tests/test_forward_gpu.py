@@ -10,6 +10,8 @@ Bars (BASELINE.json north_star), asserted as written:
 Plain single-rounding bf16 ('bf16-unsafe') carries no tolerance claim and is not tested here; its
 measured error envelope lives in tests/test_diagnostics_gpu.py.
 """
+import time
+
 import numpy as np
 import pytest
 import torch
@@ -221,9 +223,14 @@ def test_cbam_team_timeout_is_reported(arch, dtype, monkeypatch):
     m = _model(arch, "synth", dtype)
     x = torch.from_numpy(np.random.default_rng(5).uniform(0, 1, (2, 1, 1200)).astype(np.float32)).cuda()
     monkeypatch.setenv("RDN_CBAM_FORCE_MISS", "3")
+    t0 = time.perf_counter()
     with pytest.raises(_lib.EngineError, match="timed out"):
         with torch.no_grad():
             m(x)
+    dt = time.perf_counter() - t0
+    # the wait is bounded by the wall clock (cbam.hip SPIN_TICKS, 0.3 s), not by a poll count
+    print(f"{arch} {dtype}: hand-off timeout reported after {dt:.2f} s")
+    assert dt < 3.0, dt
     y = engine.forward(arch, dtype, m.packed_weights(x.device), x, check=False)
     torch.cuda.synchronize()
     assert torch.isnan(y[0]).any()
