@@ -206,26 +206,37 @@ __device__ __forceinline__ void mstep(const Frags& F, int s, V b, Acc& acc) {
 // (row, slot) item per lane and step waited on its loads ten times: 7 % of the RDN_F16MIX hybrid,
 // which runs two stems per tile); channel pairs on v_pk_fma_f32 and a packed ReLU after the rounding
 // (without ACCUM).
-// The stem's x values (rows lane + 64k, taps -1 / 0 / +1) fetched by buffer loads: positions outside
-// [0, L) read 0 by the range check of the resource.  A caller may issue them early (stem_load) and
-// hand them to the stem later, so their latency hides under other work (the RDN_F16MIX hybrid
-// fetches its left stem's inputs before the right head).
+// The stem's x values: rows lane + 64k by buffer loads (positions outside [0, L) read 0 by the range
+// check of the resource), plus the two positions just outside the tile's rows; the taps -1 / +1 come
+// from the neighbouring lanes (DPP wave shifts) in stem, so a lane issues NK + 2 loads instead of
+// 3 NK (every wave fetches the whole tile's x: one load per row, not three).  A caller may issue them
+// early (stem_load) and hand them to the stem later, so their latency hides under other work (the
+// RDN_F16MIX hybrid fetches its left stem's inputs before the right head).
 constexpr int STEM_NK = WB / 64;
 struct StemX {
-  float xm[STEM_NK], x0[STEM_NK], xp[STEM_NK];
+  float x0[STEM_NK];
+  float xe0, xe1;               // positions base - 1 and base + WB
 };
 __device__ __forceinline__ StemX stem_load(const Tile& tl) {
   StemX s;
   const int lane = tid() & 63;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)tl.x, 0, tl.L * 4, 0x00020000);
 #pragma unroll
-  for (int k = 0; k < STEM_NK; ++k) {
-    const int p = tl.base + lane + 64 * k;
-    s.xm[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (p - 1), 0, 0));
-    s.x0[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * p, 0, 0));
-    s.xp[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (p + 1), 0, 0));
-  }
+  for (int k = 0; k < STEM_NK; ++k)
+    s.x0[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (tl.base + lane + 64 * k), 0, 0));
+  s.xe0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (tl.base - 1), 0, 0));
+  s.xe1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (tl.base + WB), 0, 0));
   return s;
+}
+// x at row lane + 64k - 1 / + 1: the wave shifted by one lane, the vacated lane from the
+// neighbouring 64-row chunk (or the position outside the tile's rows)
+__device__ __forceinline__ float stem_xm(const StemX& s, int k) {
+  const float prev = k == 0 ? s.xe0 : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.x0[k - 1]), 63));
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(prev), __float_as_int(s.x0[k]), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float stem_xp(const StemX& s, int k) {
+  const float next = k == STEM_NK - 1 ? s.xe1 : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s.x0[k + 1]), 0));
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(next), __float_as_int(s.x0[k]), 0x130, 0xf, 0xf, false));
 }
 
 // Conv1d(1, 64, 3, padding=1) (+ folded BN) + ReLU in fp32.  ACCUM adds the result onto the resident
@@ -265,13 +276,14 @@ __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, co
     const int p = tl.base + row;
     const bool valid = in_range(p, tl.L);
     if (out_lo <= out_hi) outside = outside || xs.x0[k] < out_lo || xs.x0[k] > out_hi;
+    const float xmk = stem_xm(xs, k), xpk = stem_xp(xs, k);
     V* ptr = (V*)(tl.lds + dst + soff(row, g));
     V v;
     if (!ACCUM) {
       // channel pairs by v_pk_fma_f32 (each half one fmaf, same order), ReLU after the rounding
       // (rounding is monotone and keeps 0: the same value), rows outside [0, L) zeroed last
       typedef float f32x2 __attribute__((ext_vector_type(2)));
-      const f32x2 xm2 = {xs.xm[k], xs.xm[k]}, x02 = {xs.x0[k], xs.x0[k]}, xp2 = {xs.xp[k], xs.xp[k]};
+      const f32x2 xm2 = {xmk, xmk}, x02 = {xs.x0[k], xs.x0[k]}, xp2 = {xpk, xpk};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         f32x2 a = {wb[2 * q], wb[2 * q + 1]};
@@ -290,9 +302,9 @@ __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, co
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float a = wb[j];
-      a = fmaf(wm[j], xs.xm[k], a);
+      a = fmaf(wm[j], xmk, a);
       a = fmaf(w0[j], xs.x0[k], a);
-      a = fmaf(wp[j], xs.xp[k], a);
+      a = fmaf(wp[j], xpk, a);
       a = fmaxf(a, 0.f);
       a += (float)v[j];
       v[j] = (E)(valid ? a : 0.f);
