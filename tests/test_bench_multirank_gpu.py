@@ -38,6 +38,24 @@ def test_bench_two_ranks_gloo():
     assert "config2" not in rec["configs"]               # single-GPU configs run at N = 1 only
 
 
+def test_bench_gpus_flag_starts_its_own_ranks():
+    """`python bench.py --gpus 2` without a launcher starts its two ranks itself
+    (torch.distributed.run, before any GPU call) and rank 0 prints one line with n_gpus = 2; here both
+    ranks share the box's one GPU over gloo."""
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--batch", "64", "--L", "2000", "--dist-backend", "gloo", "--no-cpu-baseline", "--no-variants",
+           "--no-batch1", "--no-pipeline", "--no-configs"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 128 and rec["config"]["parallelism"] == "dp2"
+
+
 def _config4(nproc, backend, port, tmp_path, total=48, archs="RRCDNet,DSDN"):
     out = tmp_path / f"c4_{nproc}_{backend}.json"
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
