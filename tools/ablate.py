@@ -23,7 +23,7 @@ VARIANTS = {"base": "", "prev": "", "cur": "", "cur2": "", "nolds": "-DRDN_ABLAT
             "tail3": "-DRDN_F16MIX_TAIL=3", "tail4": "-DRDN_F16MIX_TAIL=4", "tail5": "-DRDN_F16MIX_TAIL=5", "nowin": "-DRDN_F16MIX_WIN=0", "nostem": "-DRDN_ABLATE_NOSTEM", "noheadv": "-DRDN_ABLATE_NOHEADV",
             "tail0": "-DRDN_F16MIX_TAIL=0", "tail2": "-DRDN_F16MIX_TAIL=2", "hybstamps": "-DRDN_HYB_STAMPS=1",
             "f6": "-DRDN_ABLATE_F6", "nocread": "-DRDN_ABLATE_NOCREAD", "nosplit": "-DRDN_ABLATE_NOSPLIT",
-            "mhead": "", "lbar": "", "stg": "", "vote": "", "comb": "", "track": "", "trk2": "", "sdpp": ""}
+            "mhead": "", "lbar": "", "stg": "", "vote": "", "comb": "", "track": "", "trk2": "", "sdpp": "", "cur": ""}
 
 
 def build():
