@@ -321,9 +321,6 @@ template <> struct Op<MODE_H8> {
     return p == 0 ? 16 * slot + 8 * half : (p == 1 ? 128 : 192) + 8 * slot + 4 * half;
   }
   __device__ static B load_b_at(const char* act, const uint32_t (&ad)[PLANES], uint32_t off) {
-#if defined(RDN_ABLATE_H8_PLAIN)        // diagnostic (tools/ablate.py): f16 only, no correction traffic
-    return B{{*(const f16x8*)(act + ad[0] + off), *(const f16x8*)(act + ad[1] + off)}, i32x8{}};
-#endif
     const i32x4v ch = *(const i32x4v*)(act + ad[2] + off), cl = *(const i32x4v*)(act + ad[3] + off);
     return B{{*(const f16x8*)(act + ad[0] + off), *(const f16x8*)(act + ad[1] + off)},
              __builtin_shufflevector(ch, cl, 0, 1, 2, 3, 4, 5, 6, 7)};
@@ -334,11 +331,7 @@ template <> struct Op<MODE_H8> {
     b.h[0] = *(const f16x8*)(act + ad[0] + off);
     b.h[1] = *(const f16x8*)(act + ad[1] + off);
     if (cin) {
-#if defined(RDN_ABLATE_NOCREAD)        // diagnostic (tools/ablate.py): no e4m3 plane reads, wrong results
-      const i32x4v ch = __builtin_bit_cast(i32x4v, b.h[0]), cl = __builtin_bit_cast(i32x4v, b.h[1]);
-#else
       const i32x4v ch = *(const i32x4v*)(act + ad[2] + off), cl = *(const i32x4v*)(act + ad[3] + off);
-#endif
       b.c = __builtin_shufflevector(ch, cl, 0, 1, 2, 3, 4, 5, 6, 7);
     }
     return b;
@@ -361,15 +354,9 @@ template <> struct Op<MODE_H8> {
   }
   __device__ static f32x4 mma(const A& a, const B& b, f32x4 acc, uint32_t sa, int s) {
     const int sb = (__builtin_amdgcn_workitem_id_x() & 32) ? H8_LO_E8M0 : H8_HI_E8M0;   // lanes 32-63: the lo blocks
-#if defined(RDN_ABLATE_F6)              // diagnostic (tools/ablate.py): the e2m3 MFMA's rate, wrong results
-    if (s == 0) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 2, 2, 0, (int)sa, 0, sb);
-    else if (s == 1) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 2, 2, 1, (int)sa, 0, sb);
-    else acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 2, 2, 2, (int)sa, 0, sb);
-#elif !defined(RDN_ABLATE_H8_PLAIN)
     if (s == 0) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 0, (int)sa, 0, sb);
     else if (s == 1) acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 1, (int)sa, 0, sb);
     else acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.c, b.c, acc, 0, 0, 2, (int)sa, 0, sb);
-#endif
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[0], b.h[0], acc, 0, 0, 0);
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a.h[1], b.h[1], acc, 0, 0, 0);
   }
@@ -479,10 +466,6 @@ __device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[Hea
   using TG = TileGeo<NBK>;
   const cfloat* hw = small_slot(tl, slot);
   if constexpr (HeadOut<MODE, NBK>::VEC) {
-#if defined(RDN_ABLATE_NOHEADV)       // diagnostic (tools/ablate.py): the vectorized head's cost, wrong output
-    for (int k = 0; k < NBK; ++k) out[k] = 0.0;
-    return;
-#endif
     const int tid = opaque_tid(), lane = tid & 63, w = tid >> 6, q = lane >> 4, c16 = lane & 15;
     // channel of element jj of 16-B f16 slot s: h16_channel order (f16 + e4m3 tile), natural otherwise
     auto chan = [&](int s, int jj) { return MODE == MODE_H8 ? h16_channel(s, jj) : 8 * s + jj; };
@@ -578,9 +561,6 @@ __device__ __forceinline__ void head(const Tile& tl, int slot, double (&out)[Hea
     for (int k = 0; k < HEAD_ROWS; ++k) {
       const int j = opaque_tid() + THREADS * k;
       out[k] = 0.0;
-#if defined(RDN_ABLATE_NOHEAD)        // diagnostic (tools/ablate.py): no head LDS traffic, wrong output
-      continue;
-#endif
       if (j >= TG::WB) continue;
       double a = (double)hw[192];
 #pragma unroll
@@ -827,24 +807,12 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
       h8_track<(EPI & RELU) != 0>(tl.amax, v);
       v = (EPI & RELU) ? h8_sat<true>(v) : h8_sat<false>(v);
       if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
-#if defined(RDN_ABLATE_NOSPLIT)         // diagnostic (tools/ablate.py): no e4m3 split VALU, wrong results
-      x[mm].hi = __builtin_convertvector(v, f16x4);
-      x[mm].hi8 = __float_as_uint(v[0]);
-      x[mm].lo8 = __float_as_uint(v[1]);
-#else
       x[mm] = h8_split(v);
-#endif
     }
     const uint32_t off = (uint32_t)(BR * j + 16 * i) * ROWB_F32;
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #if defined(RDN_ABLATE_NOSTORE)
     if (x[0].hi8 == 0x12345678u)
-#endif
-#if defined(RDN_ABLATE_H8_PLAIN)
-    {
-      *(f16x8*)(tl.lds + sadr[0][0] + off) = __builtin_shufflevector(x[0].hi, x[1].hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    }
-    if (false)
 #endif
     {
       *(f16x8*)(tl.lds + sadr[0][0] + off) = __builtin_shufflevector(x[0].hi, x[1].hi, 0, 1, 2, 3, 4, 5, 6, 7);
