@@ -188,8 +188,8 @@ class _EngineNet(nn.Module):
         if why is None and code != 0 and x.numel():
             lo, hi = torch.aminmax(x)                         # one pass, no |x| copy
             parts = [lo.reshape(1), hi.reshape(1)]
-            if ws is not None:
-                parts.append(ws.range_word().to(torch.float32))
+            if ws is not None:                                 # its bits as a float: nonzero iff set
+                parts.append(ws.range_word().view(torch.float32))
             h = torch.cat(parts).tolist()                      # the call's one host wait
             if ws is not None and h[2] != 0:
                 ws.clear_range_word()

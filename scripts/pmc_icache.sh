@@ -2,7 +2,7 @@
 set +e
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-OUT=gpurun_out/icache
+OUT=gpurun_out/r04/icache
 mkdir -p $OUT
 SHORT="bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-variants --no-pipeline --no-batch1 --no-configs --batch 4096"
 timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1
