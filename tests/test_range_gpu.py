@@ -143,7 +143,7 @@ def test_no_false_range_error_after_saturated_launch(dtype, short, inputs, monke
     with large values, then normal spectra of ragged lengths -- edge tiles with idle waves -- must run
     without RDN_ERANGE and without NaN, in both tile geometries (RDN_SHORT_TILES)."""
     import raman_mi355x as R
-    from raman_mi355x import engine
+    from raman_mi355x import _lib, engine
     monkeypatch.setenv("RDN_SHORT_TILES", short)
     sd = golden_state_dict("RRCDNet", "trained")
     m = R.RRCDNet()
@@ -156,7 +156,7 @@ def test_no_false_range_error_after_saturated_launch(dtype, short, inputs, monke
     for L in (1200, 2049, 1000, 5000, 333, 4099):
         ws_big = engine.Workspace("RRCDNet", code, big.shape[0], big.shape[-1], big.device)
         engine.forward("RRCDNet", code, packed, big, check=False, workspace=ws_big)
-        with pytest.raises(Exception):
+        with pytest.raises(_lib.RangeError):
             ws_big.check()                                       # x1000 saturates (test above)
         for B in (2, 16):
             x = torch.from_numpy(np.ascontiguousarray(np.tile(base[:, :L], (B // 2, 1)))).unsqueeze(1).cuda()
