@@ -869,10 +869,12 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
       for (int i = 0; i < NT; ++i) {
 #pragma unroll
         for (int mm = 0; mm < MT; ++mm) {
-          if constexpr (MODE == MODE_H8) {
+          if constexpr (MODE == MODE_H8 && !(EPI & (ADD_ID | SAVE_ID))) {
             // the M-tiles' chains interleaved (e4m3 MFMAs, then each f16 half): no MFMA issues right
             // behind the one whose result it adds to (+0.8 % on the hybrid, bit-equal: each chain keeps
-            // its order; the f16 MFMAs ahead of the e4m3 one cost 6 %, ablate_m.log)
+            // its order; the f16 MFMAs ahead of the e4m3 one cost 6 %, ablate_m.log).  Not on the
+            // residual convs, whose identity VGPRs leave no room for the longer live ranges (DSDN
+            // f16f8 spilled 5 more VGPRs)
             if (mm > 0) break;
             if (cin) {
 #pragma unroll
@@ -882,6 +884,8 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
             for (int u = 0; u < 2; ++u)
 #pragma unroll
               for (int m2 = 0; m2 < MT; ++m2) part[s % SP][i][m2] = O::mma_h(a[m2][s], bnext[i], part[s % SP][i][m2], u);
+          } else if constexpr (MODE == MODE_H8) {
+            part[s % SP][i][mm] = O::mma(a[mm][s], bnext[i], part[s % SP][i][mm], sc_l[mm], s, cin);
           } else {
             part[s % SP][i][mm] = O::mma(a[mm][s], bnext[i], part[s % SP][i][mm], sc_l[mm], s);
           }
