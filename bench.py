@@ -77,8 +77,9 @@ def index_blocks(world, rank, B, steps_pipeline=3, B4=8192, chunks4=4):
     pipe = (p0, p0 + (steps_pipeline + 1) * B)
     c4first = world * B + world * (steps_pipeline + 1) * B
     c4total = world * chunks4 * B4
+    # the sustained (config 3) window: a block of 2^32 indices per rank far beyond the others
     return {"headline": head, "pipeline": pipe, "config4_first": c4first, "config4_total": c4total,
-            "config4_warmup_first": c4first + c4total}
+            "config4_warmup_first": c4first + c4total, "sustained_first": (1 << 40) + rank * (1 << 32)}
 
 
 def launch_ranks(n, argv):
@@ -302,6 +303,93 @@ def time_pipeline(engine, arch, dtype, packed, seed, first, B, L, steps, stream,
             "note": "simulate -> fused forward -> fp64 metric sums per step, all on device (configs 3-4)"}
 
 
+class ClockSampler:
+    """Background sampler of the GPU's graphics clock (torch.cuda.clock_rate: amdsmi, MHz) and board
+    power (torch.cuda.power_draw) while a leg runs; empty if the query is unavailable on the box."""
+
+    def __init__(self, dev, period=0.25):
+        import threading
+        self.dev, self.period, self.clk, self.pw = dev, period, [], []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                self.clk.append(float(torch.cuda.clock_rate(self.dev)))
+            except Exception:            # noqa: BLE001 - no amdsmi / no permission: report nothing
+                return
+            try:
+                self.pw.append(float(torch.cuda.power_draw(self.dev)))
+            except Exception:            # noqa: BLE001
+                pass
+            self._stop.wait(self.period)
+
+    def __enter__(self):
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._t.join(timeout=5)
+
+    def summary(self):
+        def st(v):
+            v = [a for a in v if a > 0]
+            return {"mean": sum(v) / len(v), "min": min(v), "max": max(v), "samples": len(v)} if v else None
+        return {"gfx_clock_mhz": st(self.clk), "power_draw": st(self.pw)}
+
+
+def time_sustained(engine, arch, dtype, packed, seed, first, B, L, seconds, min_spectra, stream, dev, fl_per_spectrum,
+                   peak):
+    """the on-device simulator feeding the fused forward for >= `seconds` and
+    >= `min_spectra` distinct spectra (indices first + i*B), reported beside the short headline window:
+    spectra/s over the whole window (simulate + forward), the forward kernels' own time and roofline
+    fraction (HIP events around every forward), per-window rates (drift), and the graphics clock."""
+    clean = torch.empty((B, L), dtype=torch.float32, device=dev)
+    noisy = torch.empty((B, L), dtype=torch.float32, device=dev)
+    y = torch.empty((B, 1, L), dtype=torch.float32, device=dev)
+    steps = max(1, -(-min_spectra // B))
+    ev = lambda: torch.cuda.Event(enable_timing=True)   # noqa: E731
+    # one untimed step (pack / launch caches), then the window
+    engine.generate(B, seed, first_index=first, signal_length=L, device=dev, out=(clean, noisy))
+    engine.forward(arch, dtype, packed, noisy.view(B, 1, L), out=y, check=False)
+    torch.cuda.synchronize()
+    marks, fwd = [], []
+    t0 = time.perf_counter()
+    with ClockSampler(dev) as clk:
+        i = 0
+        while True:
+            engine.generate(B, seed, first_index=first + (i + 1) * B, signal_length=L, device=dev, out=(clean, noisy))
+            a, b = ev(), ev()
+            a.record(stream)
+            engine.forward(arch, dtype, packed, noisy.view(B, 1, L), out=y, check=False)
+            b.record(stream)
+            fwd.append((a, b))
+            i += 1
+            if i % 16 == 0:
+                torch.cuda.synchronize()
+                marks.append((i, time.perf_counter()))
+                if i >= steps and marks[-1][1] - t0 >= seconds:
+                    break
+        torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if not bool(torch.isfinite(y).all()):
+        raise RuntimeError("non-finite outputs in the sustained window")
+    ms_fwd = [a.elapsed_time(b) for a, b in fwd]
+    kms = sum(ms_fwd) / len(ms_fwd)
+    n_win = 4
+    q = max(1, len(ms_fwd) // n_win)
+    win = [sum(ms_fwd[k * q:(k + 1) * q]) / q for k in range(n_win)]
+    return {"spectra": i * B, "seconds": el, "spectra_per_s": i * B / el, "steps": i, "batch": B,
+            "forward_kernel_ms": kms, "forward_spectra_per_s": B / (kms * 1e-3),
+            "roofline_frac": fl_per_spectrum * B / (kms * 1e-3) / 1e12 / peak,
+            "forward_kernel_ms_by_quarter": win, "first_index": first,
+            **clk.summary(),
+            "note": "config 3 steady state: per step the device simulator writes B fresh spectra and the fused forward "
+                    "denoises them; forward_kernel_ms from HIP events around each forward on the launch stream"}
+
+
 def _model(R, arch, dtype, dev, trained=True):
     """Module of `arch` on `dev` with the trained golden fixture weights (or random init)."""
     torch.manual_seed(1234)
@@ -404,6 +492,9 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip timing the simulate -> forward -> metrics pipeline (SURVEY.md §8d configs 3-4)")
     ap.add_argument("--no-configs", action="store_true", help="skip the configs 2/4/5 keys")
+    ap.add_argument("--sustained-seconds", type=float, default=10.0,
+                    help="config 3 steady-state window (also >= --sustained-spectra); 0 skips it")
+    ap.add_argument("--sustained-spectra", type=int, default=2_000_000)
     ap.add_argument("--config2-n", type=int, default=1_000_000, help="config 2 spectra (1DCNN fp32)")
     ap.add_argument("--config2-batch", type=int, default=65536)
     ap.add_argument("--config4-batch", type=int, default=8192)
@@ -532,6 +623,13 @@ def main():
         pipeline = time_pipeline(engine, args.arch, code, packed, args.seed, blocks["pipeline"][0], B, L,
                                  3, stream, dev)
 
+    sustained = None
+    if args.sustained_seconds > 0:
+        progress(f"sustained: >= {args.sustained_seconds:g} s and >= {args.sustained_spectra} spectra")
+        sustained = time_sustained(engine, args.arch, code, packed, args.seed, blocks["sustained_first"], B, L,
+                                   args.sustained_seconds, args.sustained_spectra, stream, dev,
+                                   flops_per_spectrum(args.arch, L), PEAK_TFLOPS[args.dtype])
+
     configs = None
     if not args.no_configs:
         configs = config_keys(R, engine, args, dev, stream, world, rank, blocks)
@@ -561,6 +659,7 @@ def main():
             "variants": variants,
             "trained_weights": trained,
             "pipeline": pipeline,
+            "sustained": sustained,
             "configs": configs,
             "batch1": batch1,
             "metrics_mean": {k: sums[i] / sums[4] for i, k in enumerate(["MSE", "SSIM", "Smoothness", "Peak2Peak"])},

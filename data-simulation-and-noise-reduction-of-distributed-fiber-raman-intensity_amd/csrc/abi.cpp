@@ -19,10 +19,14 @@ void set_corr_mask(void* blob, uint64_t mask);
 uint64_t get_corr_mask(const void* blob);
 uint32_t get_blob_tag(const void* blob);
 uint64_t f16mix_default_mask(int arch);
-hipError_t launch_fused16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
-hipError_t launch_fused16_f16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, hipStream_t s);
+hipError_t launch_fused16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
+                          hipStream_t s);
+hipError_t launch_fused16_f16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
+                              hipStream_t s);
+hipError_t launch_fused16_f16_walk(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
+                                   unsigned* status, hipStream_t s);
 hipError_t launch_fused16_f16_small(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
-                                   hipStream_t s);
+                                   unsigned* status, hipStream_t s);
 hipError_t launch_fused_inplace_short(const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
                                       hipStream_t s);
 hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
@@ -57,9 +61,12 @@ int hip_check(hipError_t e, const char* what) {
 bool valid_arch(int a) { return a >= RDN_DENOISECNN && a <= RDN_APIDN; }
 bool valid_dtype(int d) { return d >= RDN_F32 && d <= RDN_F16MIX; }
 bool is_cbam(int a) { return a == RDN_ADSDN || a == RDN_APIDN; }
-// the dtypes whose e4m3 correction planes bound the activations (RDN_ERANGE, inplace.hpp range_vote);
-// the fused networks keep their range word in the first 4 bytes of a RANGE_WS_BYTES workspace
+// the dtypes whose e4m3 correction planes bound the activations (RDN_ERANGE, inplace.hpp range_vote)
 bool range_checked(int d) { return d == RDN_F16F8 || d == RDN_F16MIX; }
+// the fused networks' 16-bit forwards keep a status word in the first 4 bytes of a RANGE_WS_BYTES
+// workspace (common.hpp STATUS_*): the range bit of the range-checked dtypes and, for every 16-bit
+// dtype, the input gate bit raised by the stems
+bool status_word(int d) { return d != RDN_F32; }
 constexpr size_t RANGE_WS_BYTES = 256;
 const char* range_msg() {
   return "an activation left the range of the e4m3 correction planes (|v| > 1792, RDN_F16F8 / RDN_F16MIX): the "
@@ -183,7 +190,7 @@ int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes,
     return fail(RDN_EINVAL, "rdn_workspace_size: bad argument");
   if (unsupported(arch, dtype)) return fail_unsupported("rdn_workspace_size");
   *bytes = is_cbam(arch) ? rdn::cbam_workspace_bytes(arch, dtype, n, L, (hipStream_t)stream)
-                          : range_checked(dtype) ? RANGE_WS_BYTES : 0;
+                          : status_word(dtype) ? RANGE_WS_BYTES : 0;
   return RDN_OK;
   RDN_GUARD_END
 }
@@ -195,7 +202,7 @@ int rdn_workspace_init(int arch, int dtype, int64_t n, int64_t L, void* ws, size
   if (unsupported(arch, dtype)) return fail_unsupported("rdn_workspace_init");
   const hipStream_t s = (hipStream_t)stream;
   if (!is_cbam(arch)) {
-    if (!range_checked(dtype)) return RDN_OK;
+    if (!status_word(dtype)) return RDN_OK;
     if (!ws || ws_bytes < RANGE_WS_BYTES)
       return fail(RDN_ESIZE, "rdn_workspace_init: workspace too small, need " + std::to_string(RANGE_WS_BYTES) + " bytes");
     return hip_check(hipMemsetAsync(ws, 0, 4, s), "rdn_workspace_init");
@@ -219,6 +226,23 @@ static bool short_tiles(int arch, int64_t n, int64_t L, hipStream_t s) {
   return cus > 0 && 2 * n * tiles <= cus;
 }
 
+// Walk geometry (fused16_walk.hip: one workgroup walks a whole spectrum, no halo recompute) for
+// RDN_F16 on the networks that have it, when its predicted time -- rounds of the CUs x tiles per
+// spectrum x 576 rows -- is below that of the 640-row tiles (rounds x 640 rows): large batches.
+// RDN_WALK = 0 / 1 forces either geometry (tests compare the two).
+static bool walk_tiles(int arch, int64_t n, int64_t L, hipStream_t s) {
+  if (!rdn::walk_shift(arch)) return false;
+  const char* env = std::getenv("RDN_WALK");
+  if (env && (env[0] == '0' || env[0] == '1')) return env[0] == '1';
+  const int64_t cus = rdn::device_cus(rdn::stream_device(s));
+  if (cus <= 0) return false;
+  const int64_t T = rdn::H16_WB - 2 * rdn::fused_halo(arch), tiles = (L + T - 1) / T;
+  const int64_t wt = (L + rdn::walk_shift(arch) + rdn::H16_WALK_ROWS - 1) / rdn::H16_WALK_ROWS;
+  const int64_t walk_rows = (n + cus - 1) / cus * wt * rdn::H16_WALK_ROWS;
+  const int64_t tile_rows = (n * tiles + cus - 1) / cus * rdn::H16_WB;
+  return walk_rows < tile_rows;
+}
+
 int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* y, int64_t n, int64_t L, void* ws,
                 size_t ws_bytes, void* stream) {
   RDN_GUARD_BEGIN
@@ -239,13 +263,16 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
       return fail(RDN_ESIZE, "rdn_forward: workspace too small, need " + std::to_string(need) + " bytes");
     return hip_check(rdn::launch_cbam_forward(arch, dtype, blob, x, y, n, (int)L, ws, ws_bytes, s), "cbam forward");
   }
-  if (dtype == RDN_BF16) return hip_check(rdn::launch_fused16(arch, blob, x, y, n, (int)L, s), "fused bf16 forward");
-  // range word of RDN_F16F8 / RDN_F16MIX (optional: without a workspace a saturated tile still writes NaN)
-  unsigned* status = range_checked(dtype) && ws && ws_bytes >= RANGE_WS_BYTES ? (unsigned*)ws : nullptr;
+  // status word of the 16-bit dtypes (optional: without a workspace a saturated tile still writes NaN,
+  // and the input gate is not reported)
+  unsigned* status = status_word(dtype) && ws && ws_bytes >= RANGE_WS_BYTES ? (unsigned*)ws : nullptr;
+  if (dtype == RDN_BF16) return hip_check(rdn::launch_fused16(arch, blob, x, y, n, (int)L, status, s), "fused bf16 forward");
   const bool shrt = short_tiles(arch, n, L, s);
+  if (dtype == RDN_F16 && !shrt && walk_tiles(arch, n, L, s))
+    return hip_check(rdn::launch_fused16_f16_walk(arch, blob, x, y, n, (int)L, status, s), "fused f16 forward (walk)");
   if (dtype == RDN_F16)
-    return hip_check(shrt ? rdn::launch_fused16_f16_small(arch, blob, x, y, n, (int)L, s)
-                          : rdn::launch_fused16_f16(arch, blob, x, y, n, (int)L, s), "fused f16 forward");
+    return hip_check(shrt ? rdn::launch_fused16_f16_small(arch, blob, x, y, n, (int)L, status, s)
+                          : rdn::launch_fused16_f16(arch, blob, x, y, n, (int)L, status, s), "fused f16 forward");
   if (dtype == RDN_F16MIX && shrt)
     return hip_check(rdn::launch_fused_inplace_short(blob, x, y, n, (int)L, status, s), "fused f16mix forward (short tiles)");
   return hip_check(rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, status, s), "fused in-place forward");
@@ -260,13 +287,15 @@ int rdn_forward_status(int arch, int dtype, int64_t n, int64_t L, void* ws, size
   const hipStream_t s = (hipStream_t)stream;
   if (!is_cbam(arch)) {
     int rc = hip_check(hipStreamSynchronize(s), "rdn_forward_status");
-    if (rc != RDN_OK || !range_checked(dtype) || !ws || ws_bytes < RANGE_WS_BYTES) return rc;
+    if (rc != RDN_OK || !status_word(dtype) || !ws || ws_bytes < RANGE_WS_BYTES) return rc;
     unsigned w = 0;
     rc = hip_check(hipMemcpy(&w, ws, sizeof(w), hipMemcpyDeviceToHost), "rdn_forward_status");
     if (rc != RDN_OK) return rc;
     if (!w) return RDN_OK;
-    rc = hip_check(hipMemset(ws, 0, 4), "rdn_forward_status");
-    return rc != RDN_OK ? rc : fail(RDN_ERANGE, range_msg());
+    // cleared on the forwards' stream: ordered before the next forward enqueued there
+    rc = hip_check(hipMemsetAsync(ws, 0, 4, s), "rdn_forward_status");
+    // the input-gate bit is informational (the module's fp32 re-run decision): only the range bit fails
+    return rc != RDN_OK || !(w & rdn::STATUS_RANGE) ? rc : fail(RDN_ERANGE, range_msg());
   }
   if (n == 0) return hip_check(hipStreamSynchronize(s), "rdn_forward_status");
   const size_t need = rdn::cbam_workspace_bytes(arch, dtype, n, L, s);

@@ -786,6 +786,7 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
     tl.layer = 0;
     tl.corr = corr_mask(blob);
     tl.amax = 0.f;
+    tl.status = nullptr;
     LayerA<MODE> a;
     load_layer_a<MODE>(tl, 0, a);
     // stats of u -> team -> apply.  The identity rows are fetched while the team assembles; the
@@ -1754,11 +1755,11 @@ hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes
   if (e != hipSuccess) return e;
   if (tg.teams <= 0) {
     *out_of_range = w[1] != 0;
-    if (w[1]) e = hipMemset(words + 1, 0, 4);
+    if (w[1]) e = hipMemsetAsync(words + 1, 0, 4, stream);     // on the forwards' stream (ordered)
   } else {
     *timed_out = w[1] != 0;
     *out_of_range = w[2] != 0;
-    if (w[1] || w[2]) e = hipMemset(words + 1, 0, 8);
+    if (w[1] || w[2]) e = hipMemsetAsync(words + 1, 0, 8, stream);
   }
   return e;
 }

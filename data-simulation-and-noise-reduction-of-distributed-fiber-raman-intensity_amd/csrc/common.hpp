@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/raman_mi355x.h"
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -86,6 +88,16 @@ constexpr int BIG_BYTES_H8 = H8_BIAS_OFF + C * 4;                          // 50
 // activations saturated to +-1792 (= 448 * 4) neither conversion can leave the e4m3 range
 constexpr int H8_HI_E8M0 = 129, H8_LO_E8M0 = 118;
 constexpr float H8_HI_DIV = 4.0f, H8_LO_DIV = 1.0f / 512.0f, H8_SAT = 1792.0f;
+// Status word of a fused network's 16-bit forward (the first 4 bytes of its workspace, sticky until
+// read): bit 0 an e4m3 activation saturated (RDN_F16F8 / RDN_F16MIX: NaN tiles, rdn_forward_status
+// RDN_ERANGE); bit 1 an input left [-INPUT_GATE, INPUT_GATE], the 16-bit modes' domain (normalised
+// intensity; informational: the drop-in module re-runs such a batch in fp32).  The stems, which read
+// every input already, raise bit 1 with one vector atomic per tile that saw such a value.
+constexpr unsigned STATUS_RANGE = RDN_STATUS_RANGE, STATUS_GATE = RDN_STATUS_GATE;   // include/raman_mi355x.h
+constexpr float INPUT_GATE = 4.0f;
+__device__ __forceinline__ void raise_status(unsigned* status, unsigned bit) {
+  __hip_atomic_fetch_or(status, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // 16-bit single-rounding layout of fused16.hip (RDN_BF16, non-CBAM networks): the same
 // [m 4][kstep 6][lane 64][8] fragments + bias, but with the K order permuted so that element j of
@@ -94,7 +106,7 @@ constexpr float H8_HI_DIV = 4.0f, H8_LO_DIV = 1.0f / 512.0f, H8_SAT = 1792.0f;
 __host__ __device__ constexpr int h16_channel(int slot, int j) {
   return 32 * (slot >> 2) + 4 * (slot & 3) + (j & 3) + 16 * (j >> 2);
 }
-constexpr int H16_WB = 640;      // rows per fused16 tile (two 80 KiB ping-pong buffers)
+
 
 // ---- LDS image ------------------------------------------------------------------------------
 // bf16 activation buffer: ROWS x 128 B, 16-B slots XOR-swizzled by (row & 7): conflict-free
@@ -121,6 +133,12 @@ __device__ __forceinline__ uint32_t off_f32(int prow, int byte) {
 
 enum Arch : int { DENOISECNN = 0, RRCDNET = 1, DSDN = 2, ADSDN = 3, PIDN = 4, APIDN = 5 };
 enum DType : int { F32 = 0, BF16 = 1, BF16X3 = 2, F16F8 = 3, F16 = 4, F16MIX = 5 };
+
+constexpr int H16_WB = 640;      // rows per fused16 tile (two 80 KiB ping-pong buffers)
+// walk geometry (fused16_walk.hip): positions a layer advances per tile, and the cumulative shift of
+// the head (the sum of the stack's dilations after the stem); 0: no walk kernel for the network
+constexpr int H16_WALK_ROWS = 576;
+__host__ __device__ constexpr int walk_shift(int arch) { return arch == DENOISECNN ? 19 : arch == RRCDNET ? 28 : 0; }
 
 // receptive half-width (rows of halo needed on each side of a tile's outputs)
 __host__ __device__ constexpr int fused_halo(int arch) {

@@ -5,6 +5,8 @@
 #include "host_util.hpp"
 
 namespace rdn {
+
+#if !defined(H16_WALK_T)
 namespace H16_NS {
 
 // Network bodies; EDGE: the tile holds positions outside [0, L) (first/last tile of a spectrum),
@@ -111,10 +113,12 @@ H16_BODY(pidn) {
 
 #define H16_KERNEL(name, arch)                                                                            \
   __global__ __launch_bounds__(THREADS) void name(const uint8_t* __restrict__ blob, const float* __restrict__ x, \
-                                                  float* __restrict__ y, int L, int T, int tiles) {        \
+                                                  float* __restrict__ y, int L, int T, int tiles,          \
+                                                  unsigned* __restrict__ status) {                         \
     extern __shared__ __attribute__((aligned(16))) char lds[];                                             \
     int n;                                                                                                 \
     Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(arch), n);                                   \
+    tl.status = status;                                                                                    \
     if (tl.base >= 0 && tl.base + WB <= L) name##_body<false>(tl, y, n, L, T);                             \
     else name##_body<true>(tl, y, n, L, T);                                                                \
   }
@@ -126,11 +130,12 @@ H16_KERNEL(pidn, PIDN)
 
 }  // namespace H16_NS
 
-typedef void (*fused_kernel_t)(const uint8_t*, const float*, float*, int, int, int);
+typedef void (*fused_kernel_t)(const uint8_t*, const float*, float*, int, int, int, unsigned*);
 
 // Host launcher: one workgroup per (spectrum, tile); tiles along L overlap by 2*halo.
-hipError_t H16_LAUNCH(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
-                          hipStream_t stream) {
+// status: the workspace's status word (the input gate, STATUS_GATE) or NULL
+hipError_t H16_LAUNCH(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
+                      hipStream_t stream) {
   fused_kernel_t k = nullptr;
   switch (arch) {
     case DENOISECNN: k = H16_NS::denoisecnn; break;
@@ -147,9 +152,151 @@ hipError_t H16_LAUNCH(int arch, const uint8_t* blob, const float* x, float* y, i
   for (int64_t n0 = 0; n0 < n; n0 += chunk) {
     const int64_t nn = n - n0 < chunk ? n - n0 : chunk;
     hipLaunchKernelGGL(k, dim3((unsigned)(nn * tiles)), dim3(H16_NS::THREADS), H16_NS::LDS_BYTES, stream, blob,
-                       x + n0 * L, y + n0 * L, L, T, tiles);
+                       x + n0 * L, y + n0 * L, L, T, tiles, status);
   }
   return hipGetLastError();
 }
+
+#else  // H16_WALK_T
+
+namespace H16_NS {
+
+// Walk bodies (fused16.hpp "Walk instantiation"): one workgroup per spectrum walks its tiles left to
+// right.  A tile's stem writes rows [0, WB) at positions base + row (base = t WT - CG - c0: the stem
+// of a branch whose stack is shallower starts c0 positions further left, so both heads of RRCDNet end
+// at the same positions); every layer then shifts by its dilation (layer() / head()), and tl.dnext
+// names the dilation of the layer that reads it (the carry rows it needs).  The last head of a tile
+// prefetches the next tile's layer 0 into the other operand buffer (copied after the next stem) and
+// the next stem's x (StemX) is fetched before it.
+__device__ __forceinline__ void walk_start(Tile& tl, int t, int c0) {
+  tl.base = t * WT - CG - c0;
+  tl.cs_cur = tl.cs_prev = (int)CARRY_OFF;
+  tl.dn_prev = 0;
+  tl.dnext = 1;
+  tl.layer = 0;
+}
+__device__ __forceinline__ StemX walk_stem_load(const Tile& tl, int t, int c0) {
+  Tile s = tl;
+  s.base = t * WT - CG - c0;
+  return stem_load(s);
+}
+
+// 1DCNN/train.py:71-82 — conv(1->64)+ReLU, 18 x [conv+ReLU], conv(64->1); head at shift 19
+constexpr int DENOISECNN_SHIFT = walk_shift(DENOISECNN);
+static_assert(DENOISECNN_SHIFT == 18 + 1, "18 layers and the head, d = 1");
+template <bool EDGE>
+__device__ __forceinline__ void denoisecnn_tile(Tile& tl, float* y, int t, int ntiles, Frags& F0, Frags& F1, StemX& xs) {
+  walk_start(tl, t, 0);
+  stem(tl, 0, BUF0, xs);
+  F0 = F1;                            // layer 0's operands, prefetched by the last head (or the kernel)
+  lds_barrier();
+  for (int i = 0; i < 9; ++i) {
+    layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F0, F1);
+    layer<RELU, EDGE>(tl, BUF1, BUF0, 1, F1, F0);
+  }
+  const bool more = t + 1 < ntiles;
+  if (more) xs = walk_stem_load(tl, t + 1, 0);
+  float o[HN];
+  head<EDGE>(tl, BUF0, F0, F1, more, o, 0);
+  store_out_walk(tl, y, o);
+  lds_barrier();                      // the next tile's stem overwrites BUF0
+}
+
+// RRCDNet/train.py:77-98 — right (BN, d = 1) and left (dilated) branches, y = x - (r + l) / 2: both
+// heads at shift 28 (right: stem shifted by 12, 15 layers, head; left: 7 x (2, 2|1) = 27, head)
+constexpr int RRCDNET_SHIFT = walk_shift(RRCDNET), RRCDNET_RIGHT_C0 = RRCDNET_SHIFT - 16;
+static_assert(RRCDNET_SHIFT == 13 * 2 + 1 + 1, "left: 13 layers d = 2, one d = 1, the head");
+template <bool EDGE>
+__device__ __forceinline__ void rrcdnet_tile(Tile& tl, float* y, int t, int ntiles, Frags& F0, Frags& F1, StemX& xs) {
+  walk_start(tl, t, RRCDNET_RIGHT_C0);
+  stem(tl, 0, BUF0, xs);
+  F0 = F1;                            // layer 0's operands, prefetched by the last head (or the kernel)
+  lds_barrier();
+  for (int i = 0; i < 7; ++i) {
+    layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F0, F1);
+    layer<RELU, EDGE>(tl, BUF1, BUF0, 1, F1, F0);
+  }
+  layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F0, F1);
+  const StemX xl = walk_stem_load(tl, t, 0);
+  float r[HN];
+  head<EDGE>(tl, BUF1, F1, F0, true, r);
+  // left_net: conv+BN+ReLU, 7 x [conv d2 + ReLU], conv+BN+ReLU, 6 x [conv d2 + ReLU], conv(64->1)
+  tl.base = t * WT - CG;
+  tl.dn_prev = 0;                     // the stem recomputes its carry rows
+  stem(tl, 1, BUF0, xl);             // the head above reads BUF1 only
+  lds_barrier();
+  for (int i = 0; i < 7; ++i) {
+    // left layer j has d = 1 at j = 7, else 2; the head reads the last with d = 1
+    tl.dnext = 2 * i + 1 == 7 ? 1 : 2;
+    layer<RELU, EDGE>(tl, BUF0, BUF1, 2, F0, F1);
+    tl.dnext = i == 6 ? 1 : 2;
+    layer<RELU, EDGE>(tl, BUF1, BUF0, 2 * i + 1 == 7 ? 1 : 2, F1, F0);
+  }
+  tl.dnext = 1;
+  float xv[HN];
+#pragma unroll
+  for (int k = 0; k < HN; ++k) {      // the combine's x, fetched before the left head
+    const int p = tl.base - 1 + head_row(k);
+    xv[k] = head_row(k) < WB && in_range(p, tl.L) ? tl.x[p] : 0.f;
+  }
+  const bool more = t + 1 < ntiles;
+  if (more) xs = walk_stem_load(tl, t + 1, RRCDNET_RIGHT_C0);
+  float l[HN];
+  head<EDGE>(tl, BUF0, F0, F1, more, l, 0);
+#pragma unroll
+  for (int k = 0; k < HN; ++k) l[k] = xv[k] - (r[k] + l[k]) / 2.0f;
+  store_out_walk(tl, y, l);
+  lds_barrier();
+}
+
+#define H16_WALK_KERNEL(name, SHIFT, C0)                                                                   \
+  __global__ __launch_bounds__(THREADS) void name##_walk(const uint8_t* __restrict__ blob,                 \
+                                                         const float* __restrict__ x, float* __restrict__ y, \
+                                                         int L, int ntiles, unsigned* __restrict__ status) { \
+    extern __shared__ __attribute__((aligned(16))) char lds[];                                             \
+    const int n = __builtin_amdgcn_workgroup_id_x();                                                       \
+    Tile tl = init_tile(lds, blob, blob + SMALL_BYTES, x + (size_t)n * L, L, 0);                           \
+    tl.status = status;                                                                                    \
+    y += (size_t)n * L;                                                                                    \
+    Frags F0, F1;                                                                                          \
+    load_frags(tl, 0, F1);                                                                                 \
+    StemX xs = walk_stem_load(tl, 0, C0);                                                                  \
+    for (int t = 0; t < ntiles; ++t) {                                                                     \
+      if (t == 0 || (t + 1) * WT > L) name##_tile<true>(tl, y, t, ntiles, F0, F1, xs);                    \
+      else name##_tile<false>(tl, y, t, ntiles, F0, F1, xs);                                               \
+      tl.first = false;                                                                                    \
+    }                                                                                                      \
+  }
+
+H16_WALK_KERNEL(denoisecnn, DENOISECNN_SHIFT, 0)
+H16_WALK_KERNEL(rrcdnet, RRCDNET_SHIFT, RRCDNET_RIGHT_C0)
+
+}  // namespace H16_NS
+
+typedef void (*walk_kernel_t)(const uint8_t*, const float*, float*, int, int, unsigned*);
+
+// Host launcher: one workgroup per spectrum (the grid should hold many spectra per CU: a spectrum is
+// one CU's sequential walk); ntiles = ceil((L + head shift) / WT).
+hipError_t H16_LAUNCH(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
+                      hipStream_t stream) {
+  walk_kernel_t k = nullptr;
+  int shift = 0;
+  switch (arch) {
+    case DENOISECNN: k = H16_NS::denoisecnn_walk; shift = H16_NS::DENOISECNN_SHIFT; break;
+    case RRCDNET: k = H16_NS::rrcdnet_walk; shift = H16_NS::RRCDNET_SHIFT; break;
+    default: return hipErrorInvalidValue;
+  }
+  const hipError_t e = ensure_dynamic_lds((const void*)k, H16_ATTR_SLOT0 + arch, (int)H16_NS::LDS_BYTES, stream_device(stream));
+  if (e != hipSuccess) return e;
+  const int ntiles = (int)(((int64_t)L + shift + H16_NS::WT - 1) / H16_NS::WT);
+  for (int64_t n0 = 0; n0 < n; n0 += 0x7fffffff) {
+    const int64_t nn = n - n0 < 0x7fffffff ? n - n0 : 0x7fffffff;
+    hipLaunchKernelGGL(k, dim3((unsigned)nn), dim3(H16_NS::THREADS), H16_NS::LDS_BYTES, stream, blob, x + n0 * L,
+                       y + n0 * L, L, ntiles, status);
+  }
+  return hipGetLastError();
+}
+
+#endif  // H16_WALK_T
 
 }  // namespace rdn

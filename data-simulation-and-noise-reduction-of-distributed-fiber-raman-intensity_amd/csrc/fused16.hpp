@@ -64,15 +64,35 @@
 namespace rdn {
 namespace H16_NS {
 
+#if defined(H16_WALK_T)
+// Walk instantiation (fused16_walk.hip): one workgroup walks a spectrum's tiles left to right and
+// every executed MFMA row is an output row.  Layer l of a tile computes WT rows at positions shifted
+// left by its cumulative dilation c_l (row r <-> position tile_base + r - CG - c_l), so its taps read
+// rows r - 2d, r - d, r of the previous layer's buffer; the CG rows in front of the computed rows
+// carry the previous tile's last 2d rows of that layer (copied through a per-layer carry slot,
+// layer_carry).  No halo is recomputed and the workgroup's start is paid once per spectrum.
+constexpr bool WALK = true;
+constexpr int WT = H16_WALK_T;                        // positions a layer advances per tile
+constexpr int CG = 4;                                  // carry rows in front of the computed rows (2 d_max)
+constexpr int WB = CG + WT;                            // buffer rows
+constexpr int CARRY_ROWS = 88;                        // sum of 2 d over the 64-channel readers (RRCDNet: 88)
+#else
+constexpr bool WALK = false;
+constexpr int CG = 0;
 #ifdef H16_TILE_ROWS
 constexpr int WB = H16_TILE_ROWS;                     // latency instantiation (fused16_small.hip): short tiles
 #else
 constexpr int WB = H16_WB;                            // 640 rows per tile, halo included
 #endif
+constexpr int WT = WB;                                // rows a layer computes
+constexpr int CARRY_ROWS = 0;
+#endif
 constexpr int ROWB = 128;                             // 64 channels x 16 bit
 constexpr uint32_t BUF_BYTES = WB * ROWB;             // 81920
-constexpr uint32_t LDS_BYTES = 2 * BUF_BYTES;         // 163840 (640 rows): the whole LDS of a CU
 constexpr uint32_t BUF0 = 0, BUF1 = BUF_BYTES;
+constexpr uint32_t CARRY_OFF = 2 * BUF_BYTES;         // walk: the layers' carry slots
+constexpr uint32_t LDS_BYTES = CARRY_OFF + CARRY_ROWS * ROWB;   // 163840 (640 rows): the whole LDS of a CU
+static_assert(LDS_BYTES <= 163840, "LDS of one CU");
 constexpr int LAYER_BYTES = H16_LAYER_BYTES;          // [m 4][k-step 6][lane 64][8 x 16 bit] ... bias[64] f32
 constexpr int BIAS_OFF = H16_BIAS_OFF;
 #ifndef RDN_H16_PF
@@ -87,7 +107,7 @@ constexpr int WAVES = 8;
 constexpr int THREADS = 64 * WAVES;
 constexpr int MH = 2;                                 // output-channel halves (32 channels each)
 constexpr int RB = WAVES / MH;                        // row blocks
-constexpr int RW = WB / RB;                           // 160 rows per wave
+constexpr int RW = WT / RB;                           // 160 rows per wave
 constexpr int NR = 16;
 constexpr int KS = 6;                                 // 3 taps x 2 x 32 channels
 constexpr int NFRAG = 12;                             // 2 M-tiles x 6 k-steps
@@ -96,7 +116,7 @@ constexpr int HEAD_LANES = 16;
 constexpr int NT = RW / NR;                           // N-tiles per wave (10 / 5)
 constexpr int HN = (NT + MH - 1) / MH;                // head N-tiles per wave (the two halves split the rows)
 static_assert(RW % NR == 0, "rows per wave must be whole N-tiles");
-static_assert((WB % 64) == 0 && (THREADS % 64) == 0, "stem items must not straddle a slot within a wave");
+static_assert(WALK || (WB % 64) == 0, "stem rows lane + 64k cover the tile");
 
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 #if RDN_H16_F16
@@ -134,9 +154,15 @@ struct Tile {
   int layer;             // big layer whose fragments are in VGPRs
   // per-lane LDS offsets, computed once per tile (no address arithmetic at each layer's start):
   // koff[d + 2][u] = soff(r0 + d, 4u + q) for tap shift d in -2..2 (no wrap), r0 = this lane's
-  // first row ((w % RB) * RW + lane % 16)
+  // first row ((w % RB) * RW + lane % 16); walk: koff[d + 4][u] for d in -4..0, r0 = CG + ...
   int koff[5][KS / 3];
   int r0;
+  // walk only (layer_carry): the carry slot of the layer being computed (its last 2 dnext rows, for
+  // the next tile), the previous layer's slot and row count (0: none, the stem recomputes its rows),
+  // the dilation of the layer that reads this one, and whether this is the spectrum's first tile
+  int cs_cur, cs_prev, dn_prev, dnext;
+  bool first;
+  unsigned* status;      // the launch's status word (input gate, STATUS_GATE) or NULL
 };
 
 struct Frags {            // one layer's operands in VGPRs: this wave's A-fragments and folded bias
@@ -212,10 +238,10 @@ __device__ __forceinline__ void mstep(const Frags& F, int s, V b, Acc& acc) {
 // 3 NK (every wave fetches the whole tile's x: one load per row, not three).  A caller may issue them
 // early (stem_load) and hand them to the stem later, so their latency hides under other work (the
 // RDN_F16MIX hybrid fetches its left stem's inputs before the right head).
-constexpr int STEM_NK = WB / 64;
+constexpr int STEM_NK = (WB + 63) / 64;
 struct StemX {
   float x0[STEM_NK];
-  float xe0, xe1;               // positions base - 1 and base + WB
+  float xe0, xe1;               // positions base - 1 and base + 64 STEM_NK
 };
 __device__ __forceinline__ StemX stem_load(const Tile& tl) {
   StemX s;
@@ -225,7 +251,7 @@ __device__ __forceinline__ StemX stem_load(const Tile& tl) {
   for (int k = 0; k < STEM_NK; ++k)
     s.x0[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (tl.base + lane + 64 * k), 0, 0));
   s.xe0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (tl.base - 1), 0, 0));
-  s.xe1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (tl.base + WB), 0, 0));
+  s.xe1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, 4 * (tl.base + 64 * STEM_NK), 0, 0));
   return s;
 }
 // x at row lane + 64k - 1 / + 1: the wave shifted by one lane, the vacated lane from the
@@ -258,7 +284,7 @@ __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, co
 #if defined(RDN_ABLATE_NOSTEM)         // diagnostic (tools/ablate.py): the stem's cost, wrong results
   return outside;
 #endif
-  static_assert(WB % 64 == 0 && WAVES == 8, "one slot per wave, rows lane + 64k");
+  static_assert(WAVES == 8, "one slot per wave, rows lane + 64k");
   constexpr int NK = STEM_NK;
   const int g = __builtin_amdgcn_readfirstlane(tid() >> 6), lane = tid() & 63;
   float wb[8], wm[8], w0[8], wp[8];
@@ -270,6 +296,11 @@ __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, co
     w0[j] = sw[3 * c + 1];
     wp[j] = sw[3 * c + 2];
   }
+  bool over = false;              // an input beyond the 16-bit modes' domain (STATUS_GATE)
+#pragma unroll
+  for (int k = 0; k < NK; ++k) over = over || fabsf(xs.x0[k]) > INPUT_GATE;
+  // every wave reads all the tile's x: wave 0 reports
+  if (tl.status && g == 0 && __builtin_amdgcn_ballot_w64(over) != 0 && lane == 0) raise_status(tl.status, STATUS_GATE);
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     const int row = lane + 64 * k;
@@ -277,6 +308,9 @@ __device__ __forceinline__ bool stem(const Tile& tl, int sslot, uint32_t dst, co
     const bool valid = in_range(p, tl.L);
     if (out_lo <= out_hi) outside = outside || xs.x0[k] < out_lo || xs.x0[k] > out_hi;
     const float xmk = stem_xm(xs, k), xpk = stem_xp(xs, k);
+    // walk: rows beyond the buffer are not stored; ACCUM skips the carry rows in front (they hold the
+    // previous tile's rows, identity already added)
+    if (WALK && (row >= WB || (ACCUM && row < CG))) continue;
     V* ptr = (V*)(tl.lds + dst + soff(row, g));
     V v;
     if (!ACCUM) {
@@ -337,6 +371,16 @@ struct BAddr {
   int m[KS], first[U], last[U];
   __device__ __forceinline__ BAddr(const Tile& tl, uint32_t src, int dil) {
     const bool d1 = dil == 1;
+    if constexpr (WALK) {     // taps at rows r - 2d, r - d, r; the carry rows in front: no wrap
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        m[u] = (int)src + (d1 ? tl.koff[2][u] : tl.koff[0][u]);
+        m[U + u] = (int)src + (d1 ? tl.koff[3][u] : tl.koff[2][u]);
+        m[2 * U + u] = (int)src + tl.koff[4][u];
+        first[u] = last[u] = 0;
+      }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       m[u] = (int)src + (d1 ? tl.koff[1][u] : tl.koff[0][u]);
@@ -352,6 +396,7 @@ struct BAddr {
   }
   __device__ __forceinline__ int at(int n, int s) const {
     const int t = s / U, u = s % U;
+    if (WALK) return m[s] + n * NR * ROWB;
     if (n == 0 && t == 0) return first[u];
     if (n == NT - 1 && t == 2) return last[u];
     return m[s] + n * NR * ROWB;
@@ -390,6 +435,28 @@ __device__ __forceinline__ void zero_outside(const Tile& tl, uint32_t dst, int r
   }
 }
 
+// Walk: the carry rows of the layer being computed and the previous layer's carry slot.  The waves
+// of the last row block (each its channel half) (a) fill dst rows [CG - 2 dnext, CG), which the next
+// layer's taps of its first rows read, from this layer's slot, written by the previous tile (zeros
+// on the spectrum's first tile: positions < 0), and (b) save the last 2 dn_prev rows of src, the
+// previous layer's output, which this layer only reads, into that layer's slot for the next tile.
+// No wave reads dst rows [0, CG) during this layer and none writes src: no barrier of their own.
+__device__ __forceinline__ void layer_carry(Tile& tl, uint32_t src, uint32_t dst, bool has_dst) {
+  const int w = __builtin_amdgcn_readfirstlane(tid() >> 6), lane = tid() & 63;
+  if (w % RB == RB - 1) {
+    const int k = lane >> 2, g = 4 * (w / RB) + (lane & 3);
+    if (has_dst && k < 2 * tl.dnext) {
+      const V v = tl.first ? (V)((E)0) : *(const V*)(tl.lds + tl.cs_cur + k * ROWB + 16 * g);
+      *(V*)(tl.lds + dst + soff(CG - 2 * tl.dnext + k, g)) = v;
+    }
+    if (k < 2 * tl.dn_prev)
+      *(V*)(tl.lds + tl.cs_prev + k * ROWB + 16 * g) = *(const V*)(tl.lds + src + soff(CG + WT - 2 * tl.dn_prev + k, g));
+  }
+  tl.cs_prev = tl.cs_cur;
+  tl.dn_prev = tl.dnext;
+  tl.cs_cur += 2 * tl.dnext * ROWB;
+}
+
 struct NoStage {
   __device__ void put(int, f32x8, bool) {}
 };
@@ -401,7 +468,11 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   const int next = tl.layer + 1;
   asm volatile("" : "+s"(src), "+s"(dst));   // per-layer addresses: not hoisted out of a network's loop (spills)
   const BAddr ba(tl, src, dil);
-  const int pos0 = tl.base + (w % RB) * RW;
+  if constexpr (WALK) {
+    tl.base -= dil;                          // this layer's outputs: positions shifted by its dilation
+    layer_carry(tl, src, dst, true);
+  }
+  const int pos0 = tl.base + CG + (w % RB) * RW;
 
   // Idle waves of a short last tile: every row of this wave lies at position >= L + 2, beyond the
   // reach (d <= 2) of any row that matters, so it skips the layer's MFMAs and only zeroes its dst
@@ -410,7 +481,8 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   // 256-row hybrid arbitrarily large, which the range guard of its staged layer and corrected tail
   // then saw (a false RDN_ERANGE after a saturating launch on the same CUs).  Its SIMD partner wave
   // has the MFMA pipe to itself; it still fetches the next layer's operands and meets the barrier.
-  if (EDGE && pos0 >= tl.L + 2) {
+  // (walk: every row at a position >= L is zero, the same rule without the halo's reach)
+  if (EDGE && pos0 >= tl.L + (WALK ? 0 : 2)) {
     if constexpr (EPI != STAGE) zero_outside(tl, dst, pos0 - tl.base, h, lane);
     if (has_next) load_frags(tl, next, G);
     if constexpr (EPI == LINEAR_SAVE) {
@@ -445,7 +517,8 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     *p = __builtin_convertvector(v, V);
 #endif
   };
-  const int sa = (int)dst + (h ? tl.koff[2][1] : tl.koff[2][0]);     // slot 4h + q of row r0
+  constexpr int K0 = WALK ? 4 : 2;                                      // koff index of tap shift 0
+  const int sa = (int)dst + (h ? tl.koff[K0][1] : tl.koff[K0][0]);   // slot 4h + q of row r0
   auto epilogue = [&](int n, const Acc& a) {
     // positions outside [0, L): only the N-tiles that straddle 0 or L (a wave-uniform, scalar test)
     // pay the per-lane check and select; the other N-tiles of an edge tile store unmasked
@@ -519,12 +592,16 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
 // No write, no barrier; the next layer's operands stream into G.
 template <bool EDGE>
 __device__ __forceinline__ void head(Tile& tl, uint32_t src, const Frags& F, Frags& G, bool has_next,
-                                     float (&out)[HN]) {
+                                     float (&out)[HN], int next_layer = -1) {
   const int w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB;
-  const int next = tl.layer + 1;
+  const int next = next_layer >= 0 ? next_layer : tl.layer + 1;
   const BAddr ba(tl, src, 1);
-  const int pos0 = tl.base + (w % RB) * RW + NR * HN * h;
-  if (EDGE && pos0 >= tl.L + 2) {
+  if constexpr (WALK) {
+    tl.base -= 1;
+    layer_carry(tl, src, 0, false);
+  }
+  const int pos0 = tl.base + CG + (w % RB) * RW + NR * HN * h;
+  if (EDGE && pos0 >= tl.L + (WALK ? 0 : 2)) {
     if (has_next) load_frags(tl, next, G);
 #pragma unroll
     for (int j = 0; j < HN; ++j) out[j] = 0.f;
@@ -579,11 +656,17 @@ __device__ __forceinline__ Tile init_tile(char* lds, const uint8_t* blob, const 
   tl.layer = 0;
   const int t = tid();
   const int q = (t & 63) >> 4;
-  tl.r0 = ((t >> 6) % RB) * RW + (t & 15);
+  tl.r0 = CG + ((t >> 6) % RB) * RW + (t & 15);
+  constexpr int D0 = WALK ? -4 : -2;
 #pragma unroll
-  for (int d = -2; d <= 2; ++d)
+  for (int d = 0; d < 5; ++d)
 #pragma unroll
-    for (int u = 0; u < 2; ++u) tl.koff[d + 2][u] = soff(tl.r0 + d, 4 * u + q);
+    for (int u = 0; u < 2; ++u) tl.koff[d][u] = soff(tl.r0 + D0 + d, 4 * u + q);
+  tl.cs_cur = tl.cs_prev = (int)CARRY_OFF;
+  tl.dn_prev = 0;
+  tl.dnext = 1;
+  tl.first = true;
+  tl.status = nullptr;
   return tl;
 }
 
@@ -598,7 +681,7 @@ __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const 
 // skipped N-tile of an odd NT
 __device__ __forceinline__ int head_row(int j) {
   const int w = tid() >> 6, n = HN * (w / RB) + j;
-  return n < NT ? (w % RB) * RW + NR * n + (tid() & (HEAD_LANES - 1)) : WB;
+  return n < NT ? CG + (w % RB) * RW + NR * n + (tid() & (HEAD_LANES - 1)) : WB;
 }
 
 __device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, const float (&v)[HN], int halo, int T) {
@@ -608,6 +691,17 @@ __device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, const
     const int j = head_row(k);
     const int p = tl.base + j;
     if (j >= halo && j < halo + T && p < tl.L) y[(size_t)n * tl.L + p] = v[k];
+  }
+}
+
+// walk: head outputs at positions inside [0, L)
+__device__ __forceinline__ void store_out_walk(const Tile& tl, float* y, const float (&v)[HN]) {
+  if ((tid() & 63) >= HEAD_LANES) return;
+#pragma unroll
+  for (int k = 0; k < HN; ++k) {
+    const int j = head_row(k);
+    const int p = tl.base + j;
+    if (j < WB && in_range(p, tl.L)) y[p] = v[k];
   }
 }
 

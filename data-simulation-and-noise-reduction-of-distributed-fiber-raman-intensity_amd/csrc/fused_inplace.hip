@@ -267,6 +267,7 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restr
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
+  tl.status = status;
   if (!f16mix_blob_ok(blob)) return nan_outputs(tl, y, n, T);
   const int need = L - tl.base + 2;
   if (tl.base >= 0 && tl.base + TileGeo<5>::WB <= L) {
@@ -292,6 +293,7 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_short(const uint8_t* __restri
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
+  tl.status = status;
   if (!f16mix_blob_ok(blob)) return nan_outputs(tl, y, n, T);
   if (tl.base >= 0 && tl.base + TileGeo<2>::WB <= L) {
     if (!hyb256::rrcdnet_hybrid_body<false, TAIL>(tl, y, n, L, T, status))
@@ -309,6 +311,7 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_short(const uint8_t* __restri
     extern __shared__ __attribute__((aligned(16))) char lds[];                                             \
     int n;                                                                                                 \
     Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(arch), n);                                   \
+    tl.status = status;                                                                                    \
     constexpr int NBK = NetGeo<arch>::NBK;                                                                 \
     const int need = L - tl.base + 2;  /* rows up to position L + 1: short last tiles */                     \
     if (tl.base >= 0 && tl.base + TileGeo<NBK>::WB <= L) name##_body<MODE, false, NBK, TAIL>(tl, y, n, L, T, status); \

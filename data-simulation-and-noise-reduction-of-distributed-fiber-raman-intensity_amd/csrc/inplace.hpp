@@ -61,6 +61,7 @@ struct Tile {
   const float* small;
   uint64_t corr;        // MODE_H8: bit i = big layer i consumes the e4m3 correction (CORR_SLOT)
   float amax;           // MODE_H8: running max of the values h8_sat saw (range guard, h8_track)
+  unsigned* status;     // the launch's status word (input gate, STATUS_GATE) or NULL
 };
 
 __device__ __forceinline__ bool in_range(int p, int L) { return p >= 0 && p < L; }
@@ -406,6 +407,7 @@ template <int MODE, bool ACCUM = false, int NBK = 4>
 __device__ __forceinline__ void stem(Tile& tl, int slot) {
   using TG = TileGeo<NBK>;
   const cfloat* sw = small_slot(tl, slot);
+  bool over = false;              // an input beyond the 16-bit modes' domain (STATUS_GATE)
   for (int j = opaque_tid(); j < TG::WB; j += THREADS) {
   const int pr = TG::row(j);
   const int p = tl.base + j;
@@ -413,6 +415,7 @@ __device__ __forceinline__ void stem(Tile& tl, int slot) {
   const float x0 = in_range(p, tl.L) ? tl.x[p] : 0.f;
   const float xp = in_range(p + 1, tl.L) ? tl.x[p + 1] : 0.f;
   const bool valid = in_range(p, tl.L);
+  over = over || fabsf(x0) > INPUT_GATE;
 #pragma unroll
   for (int cb = 0; cb < 16; ++cb) {
     f32x4 v = ACCUM ? Op<MODE>::load4(tl.lds, pr, 4 * cb) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -430,6 +433,8 @@ __device__ __forceinline__ void stem(Tile& tl, int slot) {
     Op<MODE>::store4(tl.lds, pr, 4 * cb, v, &tl.amax);
   }
   }
+  if (tl.status && __builtin_amdgcn_ballot_w64(over) != 0 && (__builtin_amdgcn_workitem_id_x() & 63) == 0)
+    raise_status(tl.status, STATUS_GATE);
 }
 
 // Conv1d(64, 1, 3, padding=1): the head, fp32 weights, fp64 or exact-ish accumulation, rounded once
@@ -1016,6 +1021,7 @@ __device__ __forceinline__ Tile make_tile_at(char* lds, const uint8_t* blob, con
   tl.layer = 0;
   tl.corr = corr_mask(blob);
   tl.amax = 0.f;
+  tl.status = nullptr;
   return tl;
 }
 __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const float* x, int L, int T,
@@ -1039,7 +1045,7 @@ __device__ __forceinline__ bool range_vote(const Tile& tl, uint32_t vote_off, un
 #pragma unroll
   for (int k = 0; k < THREADS / 64; ++k) sat = sat || vote[k] != 0;
   __syncthreads();
-  if (sat && status && tid == 0) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (sat && status && tid == 0) raise_status(status, STATUS_RANGE);
   return sat;
 }
 // The same vote split around a caller's barrier (the RDN_F16MIX hybrid publishes it with its own
@@ -1055,8 +1061,7 @@ __device__ __forceinline__ bool range_vote_read(const Tile& tl, uint32_t vote_of
   bool sat = false;
 #pragma unroll
   for (int k = 0; k < THREADS / 64; ++k) sat = sat || vote[k] != 0;
-  if (sat && status && __builtin_amdgcn_workitem_id_x() == 0)
-    __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (sat && status && __builtin_amdgcn_workitem_id_x() == 0) raise_status(status, STATUS_RANGE);
   return sat;
 }
 template <int N>

@@ -91,6 +91,7 @@ __device__ __forceinline__ bool rrcdnet_hybrid_body(Tile& tl, float* y, int n, i
   using HO = HeadOut<MODE_H8, NBK>;
   HybStamps st;
   PPNS::Tile t16 = pp_tile(tl);
+  t16.status = tl.status;        // the right stem reads every x of the tile: the input gate
   PPNS::Frags F0, F1;            // alternating operand buffers (fused16.hpp layer)
   PPNS::load_frags(t16, 0, F0);
   const PPNS::StemX xr = PPNS::stem_load(t16);

@@ -18,7 +18,7 @@ CSRC = os.path.join(os.path.dirname(PKG), "csrc")
 HEADER = os.path.join(os.path.dirname(os.path.dirname(PKG)), "include", "raman_mi355x.h")
 
 RDN_OK = 0
-ABI_VERSION = 4
+ABI_VERSION = 5
 # exact metric accumulator words (include/raman_mi355x.h RDN_ACC_*)
 ACC_LIMBS = 6
 ACC_STRIDE = ACC_LIMBS + 1

@@ -15,8 +15,12 @@ ARCH_ID = {a: i for i, a in enumerate(ARCHS)}
 CBAM_ARCHS = ("ADSDN", "APIDN")
 CBAM_IDS = tuple(ARCH_ID[a] for a in CBAM_ARCHS)
 # dtypes whose e4m3 correction planes bound the activations (|v| <= 1792): their forwards report a
-# saturated tile through the workspace's range word (RangeError) and write NaN for it
+# saturated tile through the workspace's status word (RangeError) and write NaN for it
 RANGE_CODES = (3, 5)
+# a fused network's 16-bit forward keeps a status word in its workspace (common.hpp STATUS_*): bit 0 an
+# e4m3 activation saturated (RANGE_CODES only), bit 1 an input left [-4, 4] (the stems' input gate,
+# models.INPUT_GATE: the 16-bit modes' domain; informational, rdn_forward_status does not fail on it)
+STATUS_RANGE, STATUS_GATE = 1, 2
 # Engine arithmetic modes (include/raman_mi355x.h rdn_dtype).  Every name here except
 # "bf16-unsafe" meets its north-star tolerance on every golden fixture (fp32: 1e-5 max-relative;
 # 16-bit modes: 2e-2 max-abs).  Single-rounding bf16 does NOT (0.24 on trained RRCDNet),
@@ -167,15 +171,20 @@ def _check_out(t, name, shape, device, dtype=torch.float32):
 
 
 def needs_workspace(arch, code):
-    """A forward of (arch, code) takes a workspace: the CBAM team kernels (required) and the
-    range-checked dtypes (their range word)."""
-    return _arch(arch) in CBAM_IDS or code in RANGE_CODES
+    """A forward of (arch, code) takes a workspace: the CBAM team kernels (required) and the fused
+    networks' 16-bit dtypes (their status word: range and input gate)."""
+    return _arch(arch) in CBAM_IDS or code != 0
+
+
+def has_status_word(arch, code):
+    """Whether a workspace of (arch, code) starts with the fused networks' status word."""
+    return _arch(arch) not in CBAM_IDS and code != 0
 
 
 class Workspace:
     """Device scratch of a forward for (arch, dtype, L) on one device and stream, reused across
-    forwards: the CBAM team kernels' slots and hand-off error word, and the range word of RDN_F16F8 /
-    RDN_F16MIX.  The status words are sticky: ``check()`` waits for the stream once and raises
+    forwards: the CBAM team kernels' slots and hand-off error word, and the fused networks' 16-bit status
+    word (the range bit of RDN_F16F8 / RDN_F16MIX, the input-gate bit).  The status words are sticky: ``check()`` waits for the stream once and raises
     EngineError if any forward since the last check timed out, RangeError if one saturated the e4m3
     planes (rdn_forward_status), so a batched driver checks once at the end instead of host-syncing
     every batch."""
@@ -213,17 +222,25 @@ class Workspace:
                                                  ctypes.c_void_p(self.stream.cuda_stream)), "rdn_workspace_size")
         return sz.value
 
-    def range_word(self):
-        """The range word of a fused network's RDN_F16F8 / RDN_F16MIX workspace (its first 4 bytes,
-        rdn_forward_status's word) as a device int32 tensor, without waiting: one element of a
-        caller's single device-to-host read (models._EngineNet.forward).  A caller that reads it
-        this way clears it with clear_range_word() (rdn_forward_status reads and clears)."""
-        if self.arch in CBAM_IDS or self.code not in RANGE_CODES:
-            raise ValueError("range_word: only the fused networks' range-checked workspaces")
+    def status_word(self):
+        """The status word of a fused network's 16-bit workspace (its first 4 bytes, rdn_forward_status's
+        word: STATUS_RANGE | STATUS_GATE bits) as a device int32 tensor, without waiting.  A caller that
+        reads it this way (models._EngineNet.forward: the call's one 4-byte host read) clears it with
+        clear_status_word() (rdn_forward_status reads and clears)."""
+        if not has_status_word(self.arch, self.code):
+            raise ValueError("status_word: only the fused networks' 16-bit workspaces")
         return self.buf[:4].view(torch.int32)
 
-    def clear_range_word(self):
-        self.buf[:4].zero_()
+    def clear_status_word(self):
+        self.buf[:4].zero_()                       # on the current stream = the forwards' (fits())
+
+    def read_status(self):
+        """Wait for the workspace's stream and return its status word (0 for a CBAM workspace) without
+        clearing it (check() clears it)."""
+        if not has_status_word(self.arch, self.code):
+            return 0
+        with torch.cuda.stream(self.stream):
+            return int(self.status_word().item())
 
     def check(self):
         """Wait for the stream; raise if a CBAM hand-off of any forward since the last check timed out."""

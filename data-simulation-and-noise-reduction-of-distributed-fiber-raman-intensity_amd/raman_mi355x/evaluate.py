@@ -75,10 +75,16 @@ def _model_forward(model, x, ws):
 
 
 def _gate(model, device):
-    """Device running max of |input| for an engine module in a 16-bit mode (models.INPUT_GATE)."""
-    if not _engine_module(model) or model.engine_code == 0:
+    """Device running max of |input| for a CBAM engine module in a 16-bit mode (models.INPUT_GATE); the
+    fused networks' kernels raise the input-gate bit of their workspace's status word instead (_gate_hit)."""
+    if not _engine_module(model) or model.engine_code == 0 or engine.has_status_word(model.ARCH, model.engine_code):
         return None
     return torch.zeros((), dtype=torch.float32, device=device)
+
+
+def _gate_hit(ws):
+    """Whether a fused network's forwards since the workspace's last check saw an input beyond the gate."""
+    return ws is not None and bool(ws.read_status() & engine.STATUS_GATE)
 
 
 def _track(gate, x):
@@ -86,11 +92,12 @@ def _track(gate, x):
     torch.maximum(gate, torch.maximum(-lo, hi), out=gate)
 
 
-def _check_gate(model, gate):
+def _check_gate(model, gate, hit=False):
     from .models import INPUT_GATE
-    if gate is not None and float(gate) > INPUT_GATE:
-        raise _lib.RangeError(f"evaluate: |input| reached {float(gate):.3g}, beyond the 16-bit modes' domain "
-                              f"({INPUT_GATE}, normalised intensity); evaluate this data in 'fp32'")
+    if hit or (gate is not None and float(gate) > INPUT_GATE):
+        seen = "" if gate is None else f" (reached {float(gate):.3g})"
+        raise _lib.RangeError(f"evaluate: |input| beyond the 16-bit modes' domain{seen} ({INPUT_GATE}, normalised "
+                              f"intensity); evaluate this data in 'fp32'")
 
 
 def _workspace(model, n, L, device):
@@ -101,6 +108,10 @@ def _workspace(model, n, L, device):
 
 
 def evaluate(model, noisy_data, clean_data, batch_size=1024, device=None):
+    """evaulate.py:25-39 batched on the device.  Inputs beyond the 16-bit modes' domain (|x| > 4) or
+    activations beyond the e4m3 planes' range raise RangeError after the run (one check at the end,
+    no per-batch wait) -- unlike the module's own forward, which re-runs such a batch in fp32: evaluate
+    such data with the module in 'fp32'."""
     model.eval()
     if device is None:
         device = next(model.parameters()).device
@@ -126,12 +137,13 @@ def evaluate(model, noisy_data, clean_data, batch_size=1024, device=None):
             x = torch.as_tensor(noisy[b0:b1], dtype=torch.float32).to(device).unsqueeze(1)
             c = torch.as_tensor(clean[b0:b1], dtype=cdt).to(device)
             y = _model_forward(model, x, ws)
-            if gate is not None:
+            if gate is not None and model.uses_engine(x):
                 _track(gate, x)
             engine.metrics(y.squeeze(1), c, per_spectrum=False, acc=acc)
+    hit = _gate_hit(ws)
     if ws is not None:
         ws.check()
-    _check_gate(model, gate)
+    _check_gate(model, gate, hit)
     _all_reduce_acc(acc)
     return means_from_acc(acc)
 
@@ -184,9 +196,10 @@ def evaluate_synthetic(models, total, seed=20250410, signal_length=10000, batch_
                 if gate is not None:
                     _track(gate, noisy[:nb])
                 engine.metrics(y[:nb].view(nb, L), clean[:nb], per_spectrum=False, acc=acc)
+            hit = _gate_hit(ws)
             if ws is not None:
                 ws.check()                  # waits for the stream; raises on a timed-out hand-off / range
-            _check_gate(model, gate)
+            _check_gate(model, gate, hit)
             torch.cuda.synchronize(device)
             el = time.perf_counter() - t0
             t = torch.tensor([el], dtype=torch.float64)

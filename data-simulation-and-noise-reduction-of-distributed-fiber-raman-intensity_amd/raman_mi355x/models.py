@@ -46,7 +46,8 @@ C = 64
 # signal to [0, 1]; noise and 5-15 sigma spikes keep every simulated spectrum inside [-1, 2]).  A
 # batch whose |x| exceeds INPUT_GATE runs in fp32 instead: beyond it the 16-bit arithmetic no longer
 # tracks the reference within the bar (the activations, and their absolute rounding error, scale with
-# the input; sigmoid heads turn that into output error -- tests/test_range_gpu.py).
+# the input; sigmoid heads turn that into output error -- tests/test_range_gpu.py).  The fused
+# networks' stems test it on the device (csrc/common.hpp INPUT_GATE, the same value).
 INPUT_GATE = 4.0
 
 
@@ -146,11 +147,11 @@ class _EngineNet(nn.Module):
         return self._fp32[1]
 
     def _workspace(self, x):
-        """The cached range-status workspace of an RDN_F16F8 / RDN_F16MIX forward on a fused network
-        (256 bytes, one layout).  None otherwise: a CBAM network's team workspace depends on the device
-        geometry and the segment switch, so engine.forward makes one per call (caching allocator)."""
+        """The cached status workspace of a 16-bit forward on a fused network (256 bytes, one layout:
+        the range and input-gate bits).  None otherwise: a CBAM network's team workspace depends on the
+        device geometry and the segment switch, so engine.forward makes one per call (caching allocator)."""
         code = self._engine_code
-        if self.ARCH in engine.CBAM_ARCHS or code not in engine.RANGE_CODES:
+        if not engine.has_status_word(self.ARCH, code):
             return None
         n, L = x.shape[0], x.shape[-1]
         if self._ws is None or not self._ws.fits(self.ARCH, code, n, L, x.device):
@@ -178,24 +179,27 @@ class _EngineNet(nn.Module):
         code = self._engine_code
         why = None
         ws = self._workspace(x)
+        range_why = "activations beyond the e4m3 planes' range (|v| > 1792)"
+        gate_why = f"|input| beyond {INPUT_GATE} (outside normalised intensity)"
         try:
-            # a fused network's range word is read below together with the input gate (one wait per
-            # call); the CBAM networks check their own workspace inside engine.forward
+            # a fused network's status word is read below (the call's one 4-byte host read); the CBAM
+            # networks check their own workspace inside engine.forward
             y = engine.forward(self.ARCH, code, self.packed_weights(x.device), x, check=ws is None, workspace=ws)
         except _lib.RangeError:
             # an activation left the e4m3 planes' range: never return the NaN tiles
-            why = "activations beyond the e4m3 planes' range (|v| > 1792)"
+            why = range_why
         if why is None and code != 0 and x.numel():
-            lo, hi = torch.aminmax(x)                         # one pass, no |x| copy
-            parts = [lo.reshape(1), hi.reshape(1)]
-            if ws is not None:                                 # its bits as a float: nonzero iff set
-                parts.append(ws.range_word().view(torch.float32))
-            h = torch.cat(parts).tolist()                      # the call's one host wait
-            if ws is not None and h[2] != 0:
-                ws.clear_range_word()
-                why = "activations beyond the e4m3 planes' range (|v| > 1792)"
-            elif max(-h[0], h[1]) > INPUT_GATE:
-                why = f"|input| beyond {INPUT_GATE} (outside normalised intensity)"
+            if ws is not None:
+                # the kernels' stems raise the input-gate bit (they read every x), the corrected
+                # layers the range bit: no extra kernel, one wait
+                w = int(ws.status_word().item())
+                if w:
+                    ws.clear_status_word()
+                    why = range_why if w & engine.STATUS_RANGE else gate_why
+            else:
+                lo, hi = torch.aminmax(x)                     # CBAM networks: one pass, no |x| copy
+                if float(torch.maximum(-lo, hi)) > INPUT_GATE:
+                    why = gate_why
         if why is None:
             return y
         # the batch is re-run in exact fp32, which has neither bound

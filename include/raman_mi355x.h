@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RDN_ABI_VERSION 4
+#define RDN_ABI_VERSION 5
 
 typedef enum {
   RDN_DENOISECNN = 0, /* 1DCNN/train.py   class DenoiseCNN */
@@ -130,9 +130,17 @@ int rdn_default_correction_mask(int arch, uint64_t* mask);
 int rdn_get_correction_mask(int arch, int dtype, const void* host_blob, size_t bytes, uint64_t* mask);
 
 /* Device scratch rdn_forward takes for a batch on the device of `stream`: the CBAM networks' team
- * geometry (depends on the device's CU count and occupancy; required), RDN_F16F8 / RDN_F16MIX on the
- * fused networks 256 bytes for the range word (optional: without it a saturated tile's outputs are
- * still NaN, but rdn_forward_status cannot report it), 0 otherwise. */
+ * geometry (depends on the device's CU count and occupancy; required); every 16-bit dtype on the fused
+ * networks 256 bytes whose first 4 bytes are the status word (optional; ABI v5), 0 otherwise (RDN_F32).
+ * Status word bits, sticky until read: RDN_STATUS_RANGE an RDN_F16F8 / RDN_F16MIX activation left the
+ * e4m3 planes' range (the tile's outputs are NaN; rdn_forward_status returns RDN_ERANGE);
+ * RDN_STATUS_GATE an input value left [-4, 4], the 16-bit modes' domain (normalised intensity: every
+ * simulated spectrum lies in [-1, 2]) -- set by the kernels' stems, which read every input anyway;
+ * informational (rdn_forward_status does not fail on it): the Python module reads the word once per
+ * call and re-runs such a batch in RDN_F32.  Without the workspace a saturated tile still writes NaN,
+ * but neither bit is reported. */
+#define RDN_STATUS_RANGE 1u
+#define RDN_STATUS_GATE 2u
 int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes, void* stream);
 
 /* Prepare a newly allocated workspace for rdn_forward on `stream`: clears its status words -- the
@@ -150,7 +158,7 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
 
 /* Completion status of every rdn_forward enqueued on `stream` with this workspace since the last
  * status call (or rdn_workspace_init): waits for the stream (hipStreamSynchronize), then reads and
- * clears the workspace's sticky status words.  RDN_EHIP if a CBAM team wait timed out (co-residency
+ * clears the workspace's sticky status words (the fused networks' word: cleared on `stream`).  RDN_EHIP if a CBAM team wait timed out (co-residency
  * broken by a concurrent kernel; the affected spectra's outputs are NaN) or the stream reported an
  * error; RDN_ERANGE if an RDN_F16F8 / RDN_F16MIX activation left the e4m3 planes' range (NaN tiles;
  * for the CBAM networks the CBAM statistics of the saturated tile also reached the rest of its

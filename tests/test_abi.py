@@ -27,7 +27,7 @@ def test_exports_every_declared_symbol(lib):
     assert declared == set(_lib.EXPORTED), declared ^ set(_lib.EXPORTED)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.rdn_version() == 4
+    assert lib.rdn_version() == 5
 
 
 def test_library_built_from_these_sources(lib):
@@ -67,14 +67,16 @@ def test_every_f16_spelling_selects_the_same_arithmetic(spelling):
         engine._dtype(spelling)
 
 
-def test_range_checked_dtypes_take_a_status_workspace(lib):
-    """ABI v4: RDN_F16F8 / RDN_F16MIX on the fused networks report a saturated e4m3 plane through a
-    256-byte workspace word (rdn_forward_status: RDN_ERANGE = -6); the other fused modes need none,
-    and rdn_workspace_init refuses a too-small range workspace (no GPU call is made for these)."""
+def test_16bit_dtypes_take_a_status_workspace(lib):
+    """ABI v5: every 16-bit dtype on the fused networks takes a 256-byte workspace whose first word is
+    the status word -- RDN_F16F8 / RDN_F16MIX report a saturated e4m3 plane through its range bit
+    (rdn_forward_status: RDN_ERANGE = -6), every 16-bit dtype an input beyond [-4, 4] through its gate
+    bit; fp32 needs none, and rdn_workspace_init refuses a too-small workspace (no GPU call is made)."""
     from raman_mi355x import _lib, engine
     n = ctypes.c_size_t()
+    assert (engine.STATUS_RANGE, engine.STATUS_GATE) == (1, 2)
     for arch in (0, 1, 2, 4):
-        for code, need in ((0, 0), (2, 0), (4, 0), (1, 0), (3, 256)):
+        for code, need in ((0, 0), (2, 256), (4, 256), (1, 256), (3, 256)):
             assert lib.rdn_workspace_size(arch, code, 8, 1000, ctypes.byref(n), None) == 0
             assert n.value == need, (arch, code, n.value)
             assert engine.needs_workspace(arch, code) == (need > 0)

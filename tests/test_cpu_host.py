@@ -216,8 +216,8 @@ def _bench_module():
 @pytest.mark.parametrize("world", [1, 2, 8])
 def test_bench_index_blocks_disjoint(world):
     """bench.py's legs never re-generate each other's spectra: every rank's headline batch, pipeline
-    batches and config-4 shard (evaluate_synthetic: [first + r N/W, first + (r+1) N/W)), and the config-4
-    warm-up, are pairwise disjoint simulator index ranges for W = 1, 2, 8."""
+    batches and config-4 shard (evaluate_synthetic: [first + r N/W, first + (r+1) N/W)), the config-4
+    warm-up and the sustained (config 3) window, are pairwise disjoint simulator index ranges for W = 1, 2, 8."""
     from raman_mi355x.distributed import shard
     bench = _bench_module()
     B, B4, chunks = 8192, 8192, 4
@@ -228,6 +228,9 @@ def test_bench_index_blocks_disjoint(world):
         lo, hi = shard(b["config4_total"], r, world)
         ranges.append((b["config4_first"] + lo, b["config4_first"] + hi))
     ranges.append((b["config4_warmup_first"], b["config4_warmup_first"] + 2 * world))
+    for r in range(world):                  # the sustained window: up to 2^32 indices per rank
+        s0 = bench.index_blocks(world, r, B, 3, B4, chunks)["sustained_first"]
+        ranges.append((s0, s0 + (1 << 32)))
     ranges.sort()
     assert all(a[1] <= c[0] for a, c in zip(ranges, ranges[1:])), ranges
     assert ranges[0][0] == 0

@@ -31,7 +31,7 @@ def build():
     from concurrent.futures import ThreadPoolExecutor
     tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
     os.makedirs(OUT, exist_ok=True)
-    srcs = ["fused16.hip", "fused16_f16.hip", "fused16_small.hip", "fused_inplace.hip", "cbam.hip", "generator.hip", "metrics.hip", "abi.cpp",
+    srcs = ["fused16.hip", "fused16_f16.hip", "fused16_small.hip", "fused16_walk.hip", "fused_inplace.hip", "cbam.hip", "generator.hip", "metrics.hip", "abi.cpp",
             "pack.cpp"]
     only = sys.argv[2:]
     names = [n for n in VARIANTS if not only or n in only]
@@ -47,7 +47,7 @@ def build():
             o = os.path.join(OUT, f"{name}_{s}.o")
             cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-mcode-object-version=5",
                    "-fno-gpu-rdc", "-c", os.path.join(src_dir, s), "-o", o] + flag.split()
-            if s in ("fused16.hip", "fused16_f16.hip", "fused16_small.hip", "fused_inplace.hip", "cbam.hip") and name != "ieee":
+            if s in ("fused16.hip", "fused16_f16.hip", "fused16_small.hip", "fused16_walk.hip", "fused_inplace.hip", "cbam.hip") and name != "ieee":
                 cmd += ["-fno-honor-nans", "-mno-amdgpu-ieee"]
             if s == "generator.hip":
                 cmd += ["-ffp-contract=off"]
