@@ -27,6 +27,8 @@ hipError_t launch_fused16_f16_walk(int arch, const uint8_t* blob, const float* x
                                    unsigned* status, hipStream_t s);
 hipError_t launch_fused16_f16_small(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                    unsigned* status, hipStream_t s);
+hipError_t launch_fused_inplace_walk(const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
+                                     hipStream_t s);
 hipError_t launch_fused_inplace_short(const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
                                       hipStream_t s);
 hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
@@ -226,19 +228,21 @@ static bool short_tiles(int arch, int64_t n, int64_t L, hipStream_t s) {
   return cus > 0 && 2 * n * tiles <= cus;
 }
 
-// Walk geometry (fused16_walk.hip: one workgroup walks a whole spectrum, no halo recompute) for
-// RDN_F16 on the networks that have it, when its predicted time -- rounds of the CUs x tiles per
-// spectrum x 576 rows -- is below that of the 640-row tiles (rounds x 640 rows): large batches.
-// RDN_WALK = 0 / 1 forces either geometry (tests compare the two).
-static bool walk_tiles(int arch, int64_t n, int64_t L, hipStream_t s) {
-  if (!rdn::walk_shift(arch)) return false;
+// Walk geometry (one workgroup walks a whole spectrum, no halo recompute: fused16_walk.hip for RDN_F16
+// on DenoiseCNN / RRCDNet, 576-row tiles; rrcdnet_hybrid_walk.hpp for RDN_F16MIX, 512-row tiles) when
+// its predicted time -- rounds of the CUs x tiles per spectrum x rows per tile -- is below that of the
+// 640-row tiles (rounds x 640 rows): large batches.  RDN_WALK = 0 / 1 forces either geometry (tests
+// compare the two).
+static bool walk_tiles(int arch, int dtype, int64_t n, int64_t L, hipStream_t s) {
+  if (!rdn::walk_shift(arch) || (dtype != RDN_F16 && dtype != RDN_F16MIX)) return false;
+  const int64_t rows = dtype == RDN_F16MIX ? RDN_WALK_ROWS_MIX : rdn::H16_WALK_ROWS;
   const char* env = std::getenv("RDN_WALK");
   if (env && (env[0] == '0' || env[0] == '1')) return env[0] == '1';
   const int64_t cus = rdn::device_cus(rdn::stream_device(s));
   if (cus <= 0) return false;
   const int64_t T = rdn::H16_WB - 2 * rdn::fused_halo(arch), tiles = (L + T - 1) / T;
-  const int64_t wt = (L + rdn::walk_shift(arch) + rdn::H16_WALK_ROWS - 1) / rdn::H16_WALK_ROWS;
-  const int64_t walk_rows = (n + cus - 1) / cus * wt * rdn::H16_WALK_ROWS;
+  const int64_t wt = (L + rdn::walk_shift(arch) + rows - 1) / rows;
+  const int64_t walk_rows = (n + cus - 1) / cus * wt * rows;
   const int64_t tile_rows = (n * tiles + cus - 1) / cus * rdn::H16_WB;
   return walk_rows < tile_rows;
 }
@@ -268,11 +272,14 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
   unsigned* status = status_word(dtype) && ws && ws_bytes >= RANGE_WS_BYTES ? (unsigned*)ws : nullptr;
   if (dtype == RDN_BF16) return hip_check(rdn::launch_fused16(arch, blob, x, y, n, (int)L, status, s), "fused bf16 forward");
   const bool shrt = short_tiles(arch, n, L, s);
-  if (dtype == RDN_F16 && !shrt && walk_tiles(arch, n, L, s))
+  const bool walk = !shrt && walk_tiles(arch, dtype, n, L, s);
+  if (dtype == RDN_F16 && walk)
     return hip_check(rdn::launch_fused16_f16_walk(arch, blob, x, y, n, (int)L, status, s), "fused f16 forward (walk)");
   if (dtype == RDN_F16)
     return hip_check(shrt ? rdn::launch_fused16_f16_small(arch, blob, x, y, n, (int)L, status, s)
                           : rdn::launch_fused16_f16(arch, blob, x, y, n, (int)L, status, s), "fused f16 forward");
+  if (dtype == RDN_F16MIX && walk)
+    return hip_check(rdn::launch_fused_inplace_walk(blob, x, y, n, (int)L, status, s), "fused f16mix forward (walk)");
   if (dtype == RDN_F16MIX && shrt)
     return hip_check(rdn::launch_fused_inplace_short(blob, x, y, n, (int)L, status, s), "fused f16mix forward (short tiles)");
   return hip_check(rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, status, s), "fused in-place forward");

@@ -137,7 +137,12 @@ enum DType : int { F32 = 0, BF16 = 1, BF16X3 = 2, F16F8 = 3, F16 = 4, F16MIX = 5
 constexpr int H16_WB = 640;      // rows per fused16 tile (two 80 KiB ping-pong buffers)
 // walk geometry (fused16_walk.hip): positions a layer advances per tile, and the cumulative shift of
 // the head (the sum of the stack's dilations after the stem); 0: no walk kernel for the network
-constexpr int H16_WALK_ROWS = 576;
+#ifndef RDN_WALK_ROWS
+#define RDN_WALK_ROWS 576
+#endif
+constexpr int H16_WALK_ROWS = RDN_WALK_ROWS;
+// the RDN_F16MIX walk (rrcdnet_hybrid_walk.hpp): the in-place engine's tile is whole 128-row blocks
+#define RDN_WALK_ROWS_MIX 512
 __host__ __device__ constexpr int walk_shift(int arch) { return arch == DENOISECNN ? 19 : arch == RRCDNET ? 28 : 0; }
 
 // receptive half-width (rows of halo needed on each side of a tile's outputs)

@@ -168,18 +168,6 @@ namespace H16_NS {
 // names the dilation of the layer that reads it (the carry rows it needs).  The last head of a tile
 // prefetches the next tile's layer 0 into the other operand buffer (copied after the next stem) and
 // the next stem's x (StemX) is fetched before it.
-__device__ __forceinline__ void walk_start(Tile& tl, int t, int c0) {
-  tl.base = t * WT - CG - c0;
-  tl.cs_cur = tl.cs_prev = (int)CARRY_OFF;
-  tl.dn_prev = 0;
-  tl.dnext = 1;
-  tl.layer = 0;
-}
-__device__ __forceinline__ StemX walk_stem_load(const Tile& tl, int t, int c0) {
-  Tile s = tl;
-  s.base = t * WT - CG - c0;
-  return stem_load(s);
-}
 
 // 1DCNN/train.py:71-82 — conv(1->64)+ReLU, 18 x [conv+ReLU], conv(64->1); head at shift 19
 constexpr int DENOISECNN_SHIFT = walk_shift(DENOISECNN);
@@ -194,10 +182,11 @@ __device__ __forceinline__ void denoisecnn_tile(Tile& tl, float* y, int t, int n
     layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F0, F1);
     layer<RELU, EDGE>(tl, BUF1, BUF0, 1, F1, F0);
   }
-  const bool more = t + 1 < ntiles;
-  if (more) xs = walk_stem_load(tl, t + 1, 0);
+  // the next tile's stem inputs and layer-0 operands, fetched unconditionally (past the last tile:
+  // harmless reads), so neither xs nor F1 stays live across a tile for the loop's last iteration
+  xs = walk_stem_load(tl, t + 1, 0);
   float o[HN];
-  head<EDGE>(tl, BUF0, F0, F1, more, o, 0);
+  head<EDGE>(tl, BUF0, F0, F1, true, o, 0);
   store_out_walk(tl, y, o);
   lds_barrier();                      // the next tile's stem overwrites BUF0
 }
@@ -239,10 +228,9 @@ __device__ __forceinline__ void rrcdnet_tile(Tile& tl, float* y, int t, int ntil
     const int p = tl.base - 1 + head_row(k);
     xv[k] = head_row(k) < WB && in_range(p, tl.L) ? tl.x[p] : 0.f;
   }
-  const bool more = t + 1 < ntiles;
-  if (more) xs = walk_stem_load(tl, t + 1, RRCDNET_RIGHT_C0);
+  xs = walk_stem_load(tl, t + 1, RRCDNET_RIGHT_C0);
   float l[HN];
-  head<EDGE>(tl, BUF0, F0, F1, more, l, 0);
+  head<EDGE>(tl, BUF0, F0, F1, true, l, 0);
 #pragma unroll
   for (int k = 0; k < HN; ++k) l[k] = xv[k] - (r[k] + l[k]) / 2.0f;
   store_out_walk(tl, y, l);

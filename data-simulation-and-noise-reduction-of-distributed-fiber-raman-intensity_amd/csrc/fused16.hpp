@@ -441,20 +441,33 @@ __device__ __forceinline__ void zero_outside(const Tile& tl, uint32_t dst, int r
 // on the spectrum's first tile: positions < 0), and (b) save the last 2 dn_prev rows of src, the
 // previous layer's output, which this layer only reads, into that layer's slot for the next tile.
 // No wave reads dst rows [0, CG) during this layer and none writes src: no barrier of their own.
-__device__ __forceinline__ void layer_carry(Tile& tl, uint32_t src, uint32_t dst, bool has_dst) {
+// Split in two so that the loads' latency hides under the layer's first N-tile: carry_load before
+// the MFMA loop, carry_store after its first N-tile (then the slot bookkeeping).
+struct Carry {
+  V a, b;               // (a): the value for dst's carry row; (b): src's last row for the slot
+};
+__device__ __forceinline__ Carry carry_load(const Tile& tl, uint32_t src, bool has_dst) {
+  Carry c;
   const int w = __builtin_amdgcn_readfirstlane(tid() >> 6), lane = tid() & 63;
   if (w % RB == RB - 1) {
     const int k = lane >> 2, g = 4 * (w / RB) + (lane & 3);
-    if (has_dst && k < 2 * tl.dnext) {
-      const V v = tl.first ? (V)((E)0) : *(const V*)(tl.lds + tl.cs_cur + k * ROWB + 16 * g);
-      *(V*)(tl.lds + dst + soff(CG - 2 * tl.dnext + k, g)) = v;
-    }
-    if (k < 2 * tl.dn_prev)
-      *(V*)(tl.lds + tl.cs_prev + k * ROWB + 16 * g) = *(const V*)(tl.lds + src + soff(CG + WT - 2 * tl.dn_prev + k, g));
+    if (has_dst && k < 2 * tl.dnext)
+      c.a = tl.first ? (V)((E)0) : *(const V*)(tl.lds + tl.cs_cur + k * ROWB + 16 * g);
+    if (k < 2 * tl.dn_prev) c.b = *(const V*)(tl.lds + src + soff(CG + WT - 2 * tl.dn_prev + k, g));
+  }
+  return c;
+}
+// rowb: bytes per carry row of this layer's slot (the staged layer's outputs are 256-B plane rows)
+__device__ __forceinline__ void carry_store(Tile& tl, uint32_t dst, bool has_dst, const Carry& c, int rowb = ROWB) {
+  const int w = __builtin_amdgcn_readfirstlane(tid() >> 6), lane = tid() & 63;
+  if (w % RB == RB - 1) {
+    const int k = lane >> 2, g = 4 * (w / RB) + (lane & 3);
+    if (has_dst && k < 2 * tl.dnext) *(V*)(tl.lds + dst + soff(CG - 2 * tl.dnext + k, g)) = c.a;
+    if (k < 2 * tl.dn_prev) *(V*)(tl.lds + tl.cs_prev + k * ROWB + 16 * g) = c.b;
   }
   tl.cs_prev = tl.cs_cur;
   tl.dn_prev = tl.dnext;
-  tl.cs_cur += 2 * tl.dnext * ROWB;
+  tl.cs_cur += 2 * tl.dnext * rowb;
 }
 
 struct NoStage {
@@ -468,9 +481,14 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   const int next = tl.layer + 1;
   asm volatile("" : "+s"(src), "+s"(dst));   // per-layer addresses: not hoisted out of a network's loop (spills)
   const BAddr ba(tl, src, dil);
+  // (a) not for STAGE: its outputs go to the in-place tile, whose carry rows the caller fills
+  // (rrcdnet_hybrid_walk.hpp stage_carry) from a slot of 256-B plane rows
+  constexpr bool CA = EPI != STAGE;
+  constexpr int CROW = EPI == STAGE ? 2 * ROWB : ROWB;
+  Carry cc;
   if constexpr (WALK) {
     tl.base -= dil;                          // this layer's outputs: positions shifted by its dilation
-    layer_carry(tl, src, dst, true);
+    cc = carry_load(tl, src, CA);
   }
   const int pos0 = tl.base + CG + (w % RB) * RW;
 
@@ -483,6 +501,7 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   // has the MFMA pipe to itself; it still fetches the next layer's operands and meets the barrier.
   // (walk: every row at a position >= L is zero, the same rule without the halo's reach)
   if (EDGE && pos0 >= tl.L + (WALK ? 0 : 2)) {
+    if constexpr (WALK) carry_store(tl, dst, CA, cc, CROW);
     if constexpr (EPI != STAGE) zero_outside(tl, dst, pos0 - tl.base, h, lane);
     if (has_next) load_frags(tl, next, G);
     if constexpr (EPI == LINEAR_SAVE) {
@@ -564,6 +583,7 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
 #endif
       mstep(F, s, B[k % (PF + 1)], acc);
       if (n > 0 && s == 1) epilogue(n - 1, prev);
+      if (WALK && n == 1 && s == 0) carry_store(tl, dst, CA, cc, CROW);
 #if !defined(RDN_ABLATE_NOALOAD)
       // the next layer's operands, one buffer load every LDSTEP-th step: the vector-memory traffic
       // of the CU's 8 waves spreads over the layer
@@ -596,12 +616,14 @@ __device__ __forceinline__ void head(Tile& tl, uint32_t src, const Frags& F, Fra
   const int w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB;
   const int next = next_layer >= 0 ? next_layer : tl.layer + 1;
   const BAddr ba(tl, src, 1);
+  Carry cc;
   if constexpr (WALK) {
     tl.base -= 1;
-    layer_carry(tl, src, 0, false);
+    cc = carry_load(tl, src, false);
   }
   const int pos0 = tl.base + CG + (w % RB) * RW + NR * HN * h;
   if (EDGE && pos0 >= tl.L + (WALK ? 0 : 2)) {
+    if constexpr (WALK) carry_store(tl, 0, false, cc);
     if (has_next) load_frags(tl, next, G);
 #pragma unroll
     for (int j = 0; j < HN; ++j) out[j] = 0.f;
@@ -626,6 +648,7 @@ __device__ __forceinline__ void head(Tile& tl, uint32_t src, const Frags& F, Fra
       if (live) {
         acc.v[0] = mma(F.a[s], B[k % (PF + 1)], s == 0 ? F.bias[0] : acc.v[0]);
       }
+      if (WALK && j == 1 && s == 0) carry_store(tl, 0, false, cc);
       // the next layer's NLOAD operand loads spread over the head's K steps (operand i at step
       // i * K / NLOAD: every one is issued however few N-tiles the head has)
       if (has_next) {
@@ -692,6 +715,21 @@ __device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, const
     const int p = tl.base + j;
     if (j >= halo && j < halo + T && p < tl.L) y[(size_t)n * tl.L + p] = v[k];
   }
+}
+
+// walk: start tile t (stem row CG at position t WT - c0: a shallower branch starts c0 further left)
+__device__ __forceinline__ void walk_start(Tile& tl, int t, int c0) {
+  tl.base = t * WT - CG - c0;
+  tl.cs_cur = tl.cs_prev = (int)CARRY_OFF;
+  tl.dn_prev = 0;
+  tl.dnext = 1;
+  tl.layer = 0;
+}
+// the stem inputs of tile t (fetched ahead: their latency hides under the previous tile's last layer)
+__device__ __forceinline__ StemX walk_stem_load(const Tile& tl, int t, int c0) {
+  Tile s = tl;
+  s.base = t * WT - CG - c0;
+  return stem_load(s);
 }
 
 // walk: head outputs at positions inside [0, L)

@@ -18,6 +18,13 @@
 #define H16_TILE_ROWS 256
 #include "fused16.hpp"
 #undef H16_TILE_ROWS
+// the same on the walk geometry (512-position tiles, the in-place engine's 4 blocks): the ping-pong
+// part of the RDN_F16MIX walk (rrcdnet_hybrid_walk.hpp)
+#undef H16_NS
+#define H16_NS h16xw
+#define H16_WALK_T RDN_WALK_ROWS_MIX
+#include "fused16.hpp"
+#undef H16_WALK_T
 
 namespace rdn {
 namespace ip {
@@ -259,16 +266,15 @@ __device__ __forceinline__ bool window_outside(const Tile& tl, float lo, float h
 }
 
 // RDN_F16MIX RRCDNet: hybrid bodies on 640-row tiles, the in-place body on short last tiles; a tile
-// whose input window leaves [F16MIX_WIN_LO, F16MIX_WIN_HI] (a spike) runs every layer corrected
+// whose input window leaves [F16MIX_WIN_LO, F16MIX_WIN_HI] (a spike) runs every layer corrected.
+// Tile `id` (spectrum id / tiles, tile id % tiles) of a launch (one tile per workgroup, or the walk
+// kernel's fallback loop over a spiked spectrum's tiles).
 template <int TAIL>
-__global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restrict__ blob, const float* __restrict__ x,
-                                                          float* __restrict__ y, int L, int T, int tiles,
-                                                          unsigned* __restrict__ status) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
+__device__ __forceinline__ void rrcdnet_hybrid_tile(char* lds, const uint8_t* blob, const float* x, float* y, int L,
+                                                    int T, int tiles, unsigned* status, int64_t id) {
   int n;
-  Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
+  Tile tl = make_tile_at(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), id, n);
   tl.status = status;
-  if (!f16mix_blob_ok(blob)) return nan_outputs(tl, y, n, T);
   const int need = L - tl.base + 2;
   if (tl.base >= 0 && tl.base + TileGeo<5>::WB <= L) {
     if (!hyb640::rrcdnet_hybrid_body<false, TAIL>(tl, y, n, L, T, status))
@@ -282,6 +288,83 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restr
   } else if (!hyb640::rrcdnet_hybrid_body<true, TAIL>(tl, y, n, L, T, status)) {
     rrcdnet_f16f8_tile<true, 5>(tl, y, n, L, T, status);
   }
+}
+template <int TAIL>
+__global__ __launch_bounds__(THREADS) void rrcdnet_hybrid(const uint8_t* __restrict__ blob, const float* __restrict__ x,
+                                                          float* __restrict__ y, int L, int T, int tiles,
+                                                          unsigned* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  if (!f16mix_blob_ok(blob)) {
+    int n;
+    const Tile tl = make_tile(lds, blob, x, L, T, tiles, fused_halo(RRCDNET), n);
+    return nan_outputs(tl, y, n, T);
+  }
+  rrcdnet_hybrid_tile<TAIL>(lds, blob, x, y, L, T, tiles, status, __builtin_amdgcn_workgroup_id_x());
+}
+
+#include "rrcdnet_hybrid_walk.hpp"
+
+// Whether any input of spectrum xs lies outside [lo, hi] (workgroup-uniform; vote words at the end of
+// the LDS, behind everything the kernels use)
+__device__ __forceinline__ bool spectrum_outside(char* lds, const float* xs, int L, float lo, float hi) {
+  bool out = false;
+  if (lo <= hi) {
+    for (int p = __builtin_amdgcn_workitem_id_x(); p < L; p += THREADS) {
+      const float v = xs[p];
+      out = out || v < lo || v > hi;
+    }
+  }
+  unsigned* vote = (unsigned*)(lds + 163840) - THREADS / 64;
+  const bool wave_out = __builtin_amdgcn_ballot_w64(out) != 0;
+  if ((__builtin_amdgcn_workitem_id_x() & 63) == 0) vote[__builtin_amdgcn_workitem_id_x() >> 6] = wave_out ? 1u : 0u;
+  __syncthreads();
+  bool any = false;
+#pragma unroll
+  for (int k = 0; k < THREADS / 64; ++k) any = any || vote[k] != 0;
+  __syncthreads();
+  return any;
+}
+
+// RDN_F16MIX RRCDNet on the walk geometry: one workgroup per spectrum (rrcdnet_hybrid_walk.hpp); a
+// spectrum with a spike takes the tiled hybrid tile by tile (T, tiles: the 640-row geometry)
+template <int TAIL>
+__global__ __launch_bounds__(THREADS) void rrcdnet_hybrid_walk(const uint8_t* __restrict__ blob,
+                                                               const float* __restrict__ x, float* __restrict__ y,
+                                                               int L, int T, int tiles, int ntiles,
+                                                               unsigned* __restrict__ status) {
+  static_assert(TAIL == F16MIX_TAIL, "the walk body is written for the compiled-in tail");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int n = __builtin_amdgcn_workgroup_id_x();
+  if (!f16mix_blob_ok(blob)) {
+    for (int p = __builtin_amdgcn_workitem_id_x(); p < L; p += THREADS) y[(size_t)n * L + p] = __uint_as_float(0x7fc00000u);
+    return;
+  }
+  if (spectrum_outside(lds, x + (size_t)n * L, L, F16MIX_WIN_LO, F16MIX_WIN_HI)) {
+    for (int t = 0; t < tiles; ++t) {
+      rrcdnet_hybrid_tile<TAIL>(lds, blob, x, y, L, T, tiles, status, (int64_t)n * tiles + t);
+      __syncthreads();               // the next tile's stem overwrites what this one read last
+    }
+    return;
+  }
+  int n_;
+  Tile tl = make_tile_at(lds, blob, x, L, 0, 1, 0, n, n_);
+  tl.status = status;
+  tl.cs_cur = tl.cs_prev = tl.dn_prev = 0;
+  tl.dnext = 1;
+  tl.first = true;
+  hybw::PP::Tile t16 = hybw::PP::init_tile(lds, blob, blob + SMALL_BYTES, tl.x, L, 0);
+  t16.status = status;
+  hybw::PP::Frags F0, F1;
+  hybw::PP::load_frags(t16, 0, F1);
+  hybw::PP::StemX xs = hybw::PP::walk_stem_load(t16, 0, hybw::RIGHT_C0);
+  y += (size_t)n * L;
+  // the first tile, the interior tiles, the tiles reaching L: three straight runs of one body each (the
+  // two bodies under one per-tile branch made the register allocator spill ~160 VGPRs)
+  hybw::tile<true>(tl, t16, y, 0, ntiles, F0, F1, xs, status);
+  t16.first = false;
+  int t = 1;
+  for (; t < ntiles && (t + 1) * hybw::PP::WT <= L; ++t) hybw::tile<false>(tl, t16, y, t, ntiles, F0, F1, xs, status);
+  for (; t < ntiles; ++t) hybw::tile<true>(tl, t16, y, t, ntiles, F0, F1, xs, status);
 }
 
 // RDN_F16MIX RRCDNet on 256-row tiles (the hybrid body on h16xs + the 2-block in-place tile): the
@@ -353,6 +436,22 @@ hipError_t launch_fused_inplace_short(const uint8_t* blob, const float* x, float
     const int64_t nn = n - n0 < chunk ? n - n0 : chunk;
     hipLaunchKernelGGL(k, dim3((unsigned)(nn * tiles)), dim3(THREADS), ip::TileGeo<2>::LDS, stream, blob, x + n0 * L,
                        y + n0 * L, L, T, tiles, status);
+  }
+  return hipGetLastError();
+}
+
+// RDN_F16MIX RRCDNet on the walk geometry (ip::rrcdnet_hybrid_walk): one workgroup per spectrum
+hipError_t launch_fused_inplace_walk(const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
+                                     hipStream_t stream) {
+  const auto k = ip::rrcdnet_hybrid_walk<ip::RRCDNET_F16MIX_TAIL>;
+  const hipError_t e = ensure_dynamic_lds((const void*)k, 93, 163840, stream_device(stream));
+  if (e != hipSuccess) return e;
+  const int H = fused_halo(RRCDNET), T = ip::TileGeo<5>::WB - 2 * H, tiles = (L + T - 1) / T;
+  const int ntiles = (int)(((int64_t)L + walk_shift(RRCDNET) + RDN_WALK_ROWS_MIX - 1) / RDN_WALK_ROWS_MIX);
+  for (int64_t n0 = 0; n0 < n; n0 += 0x7fffffff) {
+    const int64_t nn = n - n0 < 0x7fffffff ? n - n0 : 0x7fffffff;
+    hipLaunchKernelGGL(k, dim3((unsigned)nn), dim3(THREADS), 163840, stream, blob, x + n0 * L, y + n0 * L, L, T, tiles,
+                       ntiles, status);
   }
   return hipGetLastError();
 }

@@ -41,6 +41,18 @@ template <int NBK> struct TileGeo {
   static constexpr uint32_t LDS = (WB + 2 * GRD) * ROWB_F32;
   __device__ static int row(int r) { return WRAP ? (r < 0 ? r + WB : (r >= WB ? r - WB : r)) : r + GRD; }
 };
+// Walk geometry (the RDN_F16MIX walk, rrcdnet_hybrid_walk.hpp; fused16.hpp "Walk instantiation"):
+// NBK blocks of computed rows behind GRD = 4 carry rows (the previous tile's last 2d rows of the
+// layer's input, taps r - 2d, r - d, r: nothing is read past the computed rows), no wrap.
+template <int NBK> struct WalkGeo {
+  static constexpr int WB = 128 * NBK;
+  static constexpr bool WRAP = false;
+  static constexpr int GRD = 4;
+  static constexpr uint32_t LDS = (WB + GRD) * ROWB_F32;
+  __device__ static int row(int r) { return r + GRD; }
+};
+template <int NBK, bool WALK> struct GeoOf { using T = TileGeo<NBK>; };
+template <int NBK> struct GeoOf<NBK, true> { using T = WalkGeo<NBK>; };
 static_assert(TileGeo<4>::LDS == LDS_BYTES, "CBAM geometry");
 static_assert(TileGeo<5>::LDS == 163840, "fused geometry fills the LDS");
 // bytes per packed big layer and offset of its bias: f32 / split-bf16 / bf16 49408 (bias at 49152),
@@ -62,6 +74,10 @@ struct Tile {
   uint64_t corr;        // MODE_H8: bit i = big layer i consumes the e4m3 correction (CORR_SLOT)
   float amax;           // MODE_H8: running max of the values h8_sat saw (range guard, h8_track)
   unsigned* status;     // the launch's status word (input gate, STATUS_GATE) or NULL
+  // walk only (conv<..., WALK>): this layer's carry slot (LDS byte offset), the previous layer's slot
+  // and its carry rows' dilation, the dilation of the layer reading this one, first tile of a spectrum
+  int cs_cur, cs_prev, dn_prev, dnext;
+  bool first;
 };
 
 __device__ __forceinline__ bool in_range(int p, int L) { return p >= 0 && p < L; }
@@ -683,14 +699,19 @@ __device__ __forceinline__ void two_sum(f32x4& hi, f32x4& c) {
 // the all-corrected kernel 18 % and the uncorrected one 38 % (measured), and a per-layer runtime
 // dispatch between instantiations inside one loop made the compiler spill 1,400-8,000 VGPRs, so a
 // mixed network is written as straight runs of one instantiation each (fused_inplace.hip).
+// WALK (WalkGeo, the RDN_F16MIX walk): taps at rows r - 2d, r - d, r, outputs dil positions further
+// left than the inputs (tl.base), and the carry rows: the last wave (a) fills the carry rows in front
+// from this layer's slot (written by the previous tile; zeros on a spectrum's first tile) once block 0,
+// their only reader, is done, and (b) saves the input's last 2 dn_prev rows into the previous layer's
+// slot for the next tile before the last block's write-back overwrites them (fused16.hpp layer_carry).
 template <int MODE, int EPI, int S, bool EDGE = true, int NBK = 4, bool CIN = true, bool COUT = true,
-          bool LOADC = true>
+          bool LOADC = true, bool WALK = false>
 __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4], LayerA<MODE>& a, bool has_next,
                                      const uint8_t* next_rec = nullptr) {
   using O = Op<MODE>;
   constexpr bool cin = MODE != MODE_H8 || CIN;
   constexpr bool cout = MODE != MODE_H8 || COUT;
-  using TG = TileGeo<NBK>;
+  using TG = typename GeoOf<NBK, WALK>::T;
   constexpr int NB = NBK, NT = IP_NT, MT = IP_MT, BR = IP_BR;
   constexpr int TS = O::KSTEPS / 3;                  // k-steps per tap
   const int tid = opaque_tid();
@@ -711,6 +732,20 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   uint32_t sc_l[MT];
 #pragma unroll
   for (int mm = 0; mm < MT; ++mm) bias_l[mm] = a.bias[mm], sc_l[mm] = a.sc[mm];
+  typedef unsigned int u32x4c __attribute__((ext_vector_type(4)));
+  u32x4c carry_a = {0u, 0u, 0u, 0u}, carry_b = {0u, 0u, 0u, 0u};
+  const bool cwave = WALK && __builtin_amdgcn_readfirstlane(tid >> 6) == THREADS / 64 - 1;
+  if constexpr (WALK) {
+    tl.base -= dil;
+    if (cwave) {                      // lane = (row k, 16-B slot): 4 rows of 256 B
+      const int k = lane >> 4, sl = lane & 15;
+      if (k < 2 * tl.dnext && !tl.first) carry_a = *(const u32x4c*)(tl.lds + tl.cs_cur + k * ROWB_F32 + 16 * sl);
+      if (k < 2 * tl.dn_prev) {
+        const int pr = TG::GRD + TG::WB - 2 * tl.dn_prev + k;
+        carry_b = *(const u32x4c*)(tl.lds + pr * ROWB_F32 + ((sl ^ swz256(pr)) << 4));
+      }
+    }
+  }
 
   // LDS byte addresses of this lane's B fragments for every k-step (row = first row of the wave's
   // share of block 0), and of its output stores; blocks and N-tiles add multiples of 16 rows,
@@ -719,7 +754,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   const int prow0 = TG::GRD + (BR / 4) * nq + c16;
 #pragma unroll
   for (int s = 0; s < O::KSTEPS; ++s) {
-    const int pr = prow0 + (O::tap(s) - 1) * dil;  // < 0 (wave 0, tap 0) only in WRAP geometry: block 0 uses bfirst
+    const int pr = prow0 + (O::tap(s) - (WALK ? 2 : 1)) * dil;  // < 0 (wave 0, tap 0) only in WRAP geometry: block 0 uses bfirst
 #pragma unroll
     for (int p = 0; p < O::PLANES; ++p) badr[s][p] = pr * ROWB_F32 + ((O::bslot(s, q, p) ^ swz256(pr)) << 4);
   }
@@ -923,6 +958,14 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
           else a[mm][s] = O::load_a(wnext, MT * mp + mm, s, lane);
         }
       }
+      if (WALK && j == 1 && s == 0 && cwave) {         // block 0 (the carry rows' reader) is done
+        const int k = lane >> 4, sl = lane & 15;
+        if (k < 2 * tl.dnext) {
+          const int pr = TG::GRD - 2 * tl.dnext + k;
+          *(u32x4c*)(tl.lds + pr * ROWB_F32 + ((sl ^ swz256(pr)) << 4)) = carry_a;
+        }
+        if (k < 2 * tl.dn_prev) *(u32x4c*)(tl.lds + tl.cs_prev + k * ROWB_F32 + 16 * sl) = carry_b;
+      }
       if (j >= 2) {
         constexpr int NP = NT * MT;
         if constexpr (MODE == MODE_H8) {
@@ -959,6 +1002,11 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   store_block(NB - 1);
   lds_barrier();                   // the layer's output is complete
   tl.layer += 1;
+  if constexpr (WALK) {
+    tl.cs_prev = tl.cs_cur;
+    tl.dn_prev = tl.dnext;
+    tl.cs_cur += 2 * tl.dnext * ROWB_F32;
+  }
 }
 
 // Conv1d(64, 1, 3) head on the MFMA for the f16 + e4m3 tile (RDN_F16MIX RRCDNet's right head): the
@@ -969,11 +1017,24 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 // which HeadOut::writer() selects.  Replaces the VALU head (48 per-lane weight loads, 16 channels x 3
 // taps of fma_mix / e4m3-decode FMAs per row and lane, a cross-quarter sum: 12.9k cycles per tile in
 // the hybrid, tools/hyb_stamps.py) by 9 MFMAs and 12 conflict-free B reads per row block.
-template <int NBK>
-__device__ __forceinline__ void head_h8_mfma(const Tile& tl, const LayerA<MODE_H8>& a, float (&out)[NBK]) {
+// WALK: taps r - 2, r - 1, r, outputs one position further left; the last wave saves the input's last
+// 2 rows into its carry slot (conv's (b)).
+template <int NBK, bool WALK = false>
+__device__ __forceinline__ void head_h8_mfma(Tile& tl, const LayerA<MODE_H8>& a, float (&out)[NBK]) {
   using O = Op<MODE_H8>;
-  using TG = TileGeo<NBK>;
+  using TG = typename GeoOf<NBK, WALK>::T;
   const int tid = opaque_tid(), lane = tid & 63, w = tid >> 6, q = lane >> 4, c16 = lane & 15;
+  if constexpr (WALK) {
+    tl.base -= 1;
+    if (__builtin_amdgcn_readfirstlane(w) == THREADS / 64 - 1) {
+      typedef unsigned int u32x4c __attribute__((ext_vector_type(4)));
+      const int k = lane >> 4, sl = lane & 15;
+      if (k < 2 * tl.dn_prev) {
+        const int pr = TG::GRD + TG::WB - 2 * tl.dn_prev + k;
+        *(u32x4c*)(tl.lds + tl.cs_prev + k * ROWB_F32 + 16 * sl) = *(const u32x4c*)(tl.lds + pr * ROWB_F32 + ((sl ^ swz256(pr)) << 4));
+      }
+    }
+  }
   f32x4 acc[NBK];
 #pragma unroll
   for (int k = 0; k < NBK; ++k) acc[k] = a.bias[0];
@@ -981,7 +1042,7 @@ __device__ __forceinline__ void head_h8_mfma(const Tile& tl, const LayerA<MODE_H
   for (int s = 0; s < O::KSTEPS; ++s) {
 #pragma unroll
     for (int k = 0; k < NBK; ++k) {
-      const typename O::B b = O::load_b(tl.lds, TG::row(128 * k + 16 * w + c16 + s - 1), s, q);
+      const typename O::B b = O::load_b(tl.lds, TG::row(128 * k + 16 * w + c16 + s - (WALK ? 2 : 1)), s, q);
       acc[k] = O::mma(a.v[0][s], b, acc[k], a.sc[0], s);
     }
   }

@@ -258,7 +258,11 @@ def forward(arch, dtype, packed, x, out=None, check=True, workspace=None):
     (rdn_forward_status).  A batched caller passes one ``Workspace`` to every forward with
     ``check=False`` and calls ``workspace.check()`` once at the end (the status words are sticky);
     ``check=False`` without a workspace keeps the launch asynchronous and unchecked (benchmarks: the
-    affected outputs are NaN)."""
+    affected outputs are NaN).  On the CBAM networks (ADSDN / APIDN) a saturated tile is NaN, but its
+    clamped CBAM statistics have already reached the other tiles of its spectrum through the team
+    hand-off: those outputs are finite and wrong.  There the status word (RangeError from ``check`` or
+    ``Workspace.check()``), not the absence of NaN, is the authoritative signal -- never run a CBAM
+    network with ``check=False`` and no later ``Workspace.check()`` on data that might saturate."""
     _check_cuda_f32(x, "input")
     if x.dim() == 3 and x.shape[1] != 1:
         raise ValueError(f"expected (N, 1, L) input, got {tuple(x.shape)}")

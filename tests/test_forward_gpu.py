@@ -136,12 +136,10 @@ def test_ragged_lengths_vs_oracle(arch, L, dtype, monkeypatch):
 @pytest.mark.parametrize("arch,which", _cases(WALK))
 def test_walk_within_tolerance(arch, which, dtype, inputs, monkeypatch):
     """The walk geometry against the reference fp32 forward on every golden input set (L = 7 ... 16384),
-    the bar of test_16bit_within_tolerance ('f16-plain' on RRCDNet only on the synthetic weights: plain
-    f16 misses 2e-2 on the trained ones)."""
+    the bar of test_16bit_within_tolerance ('f16' on RRCDNet = the RDN_F16MIX walk; 'f16-plain' on
+    RRCDNet only on the synthetic weights: plain f16 misses 2e-2 on the trained ones)."""
     if dtype == "f16-plain-walk" and (arch != "RRCDNet" or which != "synth"):
         pytest.skip("plain f16 RRCDNet is held to the bar on the synthetic weights only")
-    if dtype == "f16-walk" and arch == "RRCDNet":
-        pytest.skip("'f16' on RRCDNet is RDN_F16MIX (the hybrid): no walk kernel")
     g = load_golden(arch)
     m = _model(arch, which, _tiles(dtype, monkeypatch))
     for name in INPUT_SETS:
@@ -172,6 +170,60 @@ def test_walk_bitwise_equal_to_tiles(arch, L, monkeypatch):
     bad = np.argwhere(y_walk != y_tiles)
     assert bad.size == 0, f"{arch} L={L}: {len(bad)} positions differ, first {bad[:5].tolist()}, " \
                           f"max {np.abs(y_walk - y_tiles).max():.3e}"
+
+
+def _f16mix_tiles_T(L):
+    return 640 - 2 * 29, -(-L // (640 - 2 * 29))
+
+
+@pytest.mark.parametrize("L", [1, 2, 7, 29, 30, 483, 484, 485, 511, 512, 513, 540, 541, 1023, 1024, 1025, 1164, 3001,
+                               10000, 16384])
+def test_walk_f16mix_matches_tiles(L, monkeypatch):
+    """The RDN_F16MIX walk (rrcdnet_hybrid_walk.hpp) runs every layer with the tiled hybrid's operands
+    and MFMA order: bitwise equal to the 640-row hybrid on every position its full hybrid tiles own (its
+    short last tile runs the in-place body with its VALU right head: there within the 16-bit bar), on
+    spectra inside the spike window; the trained fixture weights."""
+    from conftest import golden_state_dict
+    import raman_mi355x as R
+    m = R.RRCDNet()
+    m.load_state_dict(golden_state_dict("RRCDNet", "trained"), strict=True)
+    m = m.cuda().eval().set_engine_dtype("f16")
+    x = np.random.default_rng(L + 1).uniform(-0.2, 1.2, (3, L)).astype(np.float32)
+    monkeypatch.setenv("RDN_SHORT_TILES", "0")
+    monkeypatch.setenv("RDN_WALK", "0")
+    y_tiles = _run(m, x)
+    monkeypatch.setenv("RDN_WALK", "1")
+    y_walk = _run(m, x)
+    assert np.isfinite(y_walk).all()
+    T, tiles = _f16mix_tiles_T(L)
+    full = (tiles - 1) * T if L - (tiles - 1) * T + 29 + 2 <= 512 else L     # positions of full hybrid tiles
+    bad = np.argwhere(y_walk[:, :full] != y_tiles[:, :full])
+    assert bad.size == 0, f"L={L}: {len(bad)} positions differ, first {bad[:5].tolist()}"
+    # the short last tile's in-place body (VALU right head, a left head on the e4m3-lo plane) against the
+    # walk's hybrid arithmetic: both within the 16-bit bar of the reference (test_walk_within_tolerance)
+    assert float(np.abs(y_walk - y_tiles).max()) <= BF16_ABS
+
+
+def test_walk_f16mix_spiked_spectra_take_the_tiles(monkeypatch):
+    """A spectrum with an input outside the spike window ([-0.3, 1.3]) runs the tiled hybrid tile by tile
+    inside the walk kernel (its spiked tiles all-corrected): bitwise equal to the tiled kernel; its
+    neighbours in the batch walk."""
+    from conftest import golden_state_dict
+    import raman_mi355x as R
+    m = R.RRCDNet()
+    m.load_state_dict(golden_state_dict("RRCDNet", "trained"), strict=True)
+    m = m.cuda().eval().set_engine_dtype("f16")
+    x = np.random.default_rng(9).uniform(0.0, 1.0, (4, 5000)).astype(np.float32)
+    x[1, 2000:2050] += 1.5                                    # a spike
+    x[3, 4990:] -= 0.9
+    monkeypatch.setenv("RDN_SHORT_TILES", "0")
+    monkeypatch.setenv("RDN_WALK", "0")
+    y_tiles = _run(m, x)
+    monkeypatch.setenv("RDN_WALK", "1")
+    y_walk = _run(m, x)
+    assert np.array_equal(y_walk[[1, 3]], y_tiles[[1, 3]])
+    T, tiles = _f16mix_tiles_T(5000)
+    assert np.array_equal(y_walk[[0, 2], :(tiles - 1) * T], y_tiles[[0, 2], :(tiles - 1) * T])
 
 
 def test_walk_large_batch_default(monkeypatch):

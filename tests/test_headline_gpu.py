@@ -13,7 +13,8 @@ own workload and on data its tuning never saw.
   Bars as in test_forward_gpu.py: 16-bit max-abs <= 2e-2 (trained weights), fp32 max-rel <= 1e-5.
 * Many-workgroup batch independence: a spectrum computed alone equals the same spectrum inside a
   300-spectrum batch (5400 workgroups, every CU busy several times over), bitwise, and the batch is
-  bitwise reproducible (the hybrid parks right-head rows in y and re-reads them, rrcdnet_hybrid.hpp).
+  bitwise reproducible (the hybrid keeps each tile's right-head rows in VGPRs over the left branch,
+  rrcdnet_hybrid.hpp; no tile reads another tile's outputs).
 * The bench workload itself: on-device simulator inputs at L = 10,000, batch 8192, random-init
   weights seeded as bench.py seeds them; a sample of spectra (first, middle, last workgroups)
   against the CPU oracle.
@@ -105,6 +106,24 @@ def test_heldout_fp32_matches_reference(which):
               f"(the reference itself {ref_own:.2e} from exact)")
         assert rel64 <= F32_REL
         assert rel <= F32_REL + ref_own
+
+
+@pytest.mark.xfail(reason="known miss (DESIGN.md §4): on the 200-epoch RRCDNet the reference's own fp32 CPU forward "
+                          "is 1.49e-5 from exact, the engine's 8.4e-6; they differ by 1.44e-5 > 1e-5", strict=False)
+def test_heldout2_fp32_plain_bar_against_fp32_reference():
+    """The north-star fp32 bar exactly as written -- max-rel <= 1e-5 against the reference's fp32
+    forward -- on the held-out RRCDNet.  It is NOT met there (the engine is within 1e-5 of the exact
+    float64 forward, test_heldout_fp32_matches_reference, and closer to it than the reference is);
+    kept as an expected failure so the measured miss stays visible in every run."""
+    g, sd = _heldout("heldout2")
+    m = _model(sd, "fp32")
+    worst = 0.0
+    for name in ("main", "odd"):
+        ref = g[f"ref_{name}"]
+        y = _run(m, g[f"in_{name}"])
+        worst = max(worst, float(np.abs(y - ref).max()) / float(np.abs(ref).max()))
+    print(f"heldout2: fp32 max-rel {worst:.2e} vs the fp32 reference (bar {F32_REL})")
+    assert worst <= F32_REL
 
 
 def test_heldout2_config1_thousand_spectra():
