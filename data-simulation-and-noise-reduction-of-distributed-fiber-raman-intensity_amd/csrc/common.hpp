@@ -142,7 +142,9 @@ constexpr int H16_WB = 640;      // rows per fused16 tile (two 80 KiB ping-pong 
 #endif
 constexpr int H16_WALK_ROWS = RDN_WALK_ROWS;
 // the RDN_F16MIX walk (rrcdnet_hybrid_walk.hpp): the in-place engine's tile is whole 128-row blocks
-#define RDN_WALK_ROWS_MIX 512
+#ifndef RDN_WALK_ROWS_MIX
+#define RDN_WALK_ROWS_MIX 576
+#endif
 __host__ __device__ constexpr int walk_shift(int arch) { return arch == DENOISECNN ? 19 : arch == RRCDNET ? 28 : 0; }
 
 // receptive half-width (rows of halo needed on each side of a tile's outputs)

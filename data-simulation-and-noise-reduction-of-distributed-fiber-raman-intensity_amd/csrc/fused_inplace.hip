@@ -358,13 +358,15 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid_walk(const uint8_t* __
   hybw::PP::load_frags(t16, 0, F1);
   hybw::PP::StemX xs = hybw::PP::walk_stem_load(t16, 0, hybw::RIGHT_C0);
   y += (size_t)n * L;
+  hybw::Stamps st;
   // the first tile, the interior tiles, the tiles reaching L: three straight runs of one body each (the
   // two bodies under one per-tile branch made the register allocator spill ~160 VGPRs)
-  hybw::tile<true>(tl, t16, y, 0, ntiles, F0, F1, xs, status);
+  hybw::tile<true>(tl, t16, y, 0, ntiles, F0, F1, xs, status, st);
   t16.first = false;
   int t = 1;
-  for (; t < ntiles && (t + 1) * hybw::PP::WT <= L; ++t) hybw::tile<false>(tl, t16, y, t, ntiles, F0, F1, xs, status);
-  for (; t < ntiles; ++t) hybw::tile<true>(tl, t16, y, t, ntiles, F0, F1, xs, status);
+  for (; t < ntiles && (t + 1) * hybw::PP::WT <= L; ++t) hybw::tile<false>(tl, t16, y, t, ntiles, F0, F1, xs, status, st);
+  for (; t < ntiles; ++t) hybw::tile<true>(tl, t16, y, t, ntiles, F0, F1, xs, status, st);
+  st.flush(status);
 }
 
 // RDN_F16MIX RRCDNet on 256-row tiles (the hybrid body on h16xs + the 2-block in-place tile): the

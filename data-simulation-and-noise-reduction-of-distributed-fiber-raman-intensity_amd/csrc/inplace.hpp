@@ -36,6 +36,7 @@ constexpr uint32_t LDS_BYTES = ACT_BYTES_F32;                    // 132096 (512 
 // by the write-backs of edge tiles.
 template <int NBK> struct TileGeo {
   static constexpr int WB = 128 * NBK;
+  static constexpr bool HALF = false;
   static constexpr bool WRAP = NBK != 4;
   static constexpr int GRD = WRAP ? 0 : GUARD;
   static constexpr uint32_t LDS = (WB + 2 * GRD) * ROWB_F32;
@@ -44,8 +45,12 @@ template <int NBK> struct TileGeo {
 // Walk geometry (the RDN_F16MIX walk, rrcdnet_hybrid_walk.hpp; fused16.hpp "Walk instantiation"):
 // NBK blocks of computed rows behind GRD = 4 carry rows (the previous tile's last 2d rows of the
 // layer's input, taps r - 2d, r - d, r: nothing is read past the computed rows), no wrap.
+// WB = RDN_WALK_ROWS_MIX computed rows in NBK blocks; when WB = 128 NBK - 64 the last block is half
+// (HALF): its rows are those of the waves of quarters nq = 0, 1, and the waves of quarters 2, 3 skip it.
 template <int NBK> struct WalkGeo {
-  static constexpr int WB = 128 * NBK;
+  static constexpr int WB = RDN_WALK_ROWS_MIX;
+  static constexpr bool HALF = WB == 128 * NBK - 64;
+  static_assert(WB == 128 * NBK || HALF, "whole blocks, or a last half block");
   static constexpr bool WRAP = false;
   static constexpr int GRD = 4;
   static constexpr uint32_t LDS = (WB + GRD) * ROWB_F32;
@@ -732,6 +737,8 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   uint32_t sc_l[MT];
 #pragma unroll
   for (int mm = 0; mm < MT; ++mm) bias_l[mm] = a.bias[mm], sc_l[mm] = a.sc[mm];
+  // WalkGeo HALF: the waves of quarters 2, 3 have no rows in the last block (wave-uniform)
+  const bool half_idle = TG::HALF && (__builtin_amdgcn_readfirstlane(tid >> 6) >> 1) >= 2;
   typedef unsigned int u32x4c __attribute__((ext_vector_type(4)));
   u32x4c carry_a = {0u, 0u, 0u, 0u}, carry_b = {0u, 0u, 0u, 0u};
   const bool cwave = WALK && __builtin_amdgcn_readfirstlane(tid >> 6) == THREADS / 64 - 1;
@@ -861,6 +868,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
     }
   };
   auto store_block = [&](int j) {
+    if (j == NB - 1 && half_idle) return;
     if constexpr (MODE == MODE_H8) {
 #pragma unroll
       for (int i = 0; i < NT; ++i) store_pair(j, i);
@@ -881,6 +889,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   for (int i = 0; i < NT; ++i) bnext[i] = read_b(0, 0, i);
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
+    const bool skip = j == NB - 1 && half_idle;       // no rows of this wave in the half block
     f32x4 part[SP][NT][MT];
     f32x4 hi[COMP ? NT : 1][COMP ? MT : 1];          // COMP: running total, starts at the bias
 #pragma unroll
@@ -907,6 +916,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
     for (int s = 0; s < O::KSTEPS; ++s) {
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
+        if (!skip) {
 #pragma unroll
         for (int mm = 0; mm < MT; ++mm) {
           if constexpr (MODE == MODE_H8 && !(EPI & (ADD_ID | SAVE_ID))) {
@@ -931,7 +941,8 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
           }
         }
         if (s + 1 < O::KSTEPS) bnext[i] = read_b(j, s + 1, i);
-        else if (j + 1 < NB) bnext[i] = read_b(j + 1, 0, i);
+        else if (j + 1 < NB && !(j + 1 == NB - 1 && half_idle)) bnext[i] = read_b(j + 1, 0, i);
+        }
         if constexpr (COMP) {
           // fold a finished chunk into the running totals (the rounding error becomes the next
           // chunk's accumulator start), staggered by one N-tile so that the VALU neither waits for
@@ -1038,10 +1049,13 @@ __device__ __forceinline__ void head_h8_mfma(Tile& tl, const LayerA<MODE_H8>& a,
   f32x4 acc[NBK];
 #pragma unroll
   for (int k = 0; k < NBK; ++k) acc[k] = a.bias[0];
+  // WalkGeo HALF: waves 4-7 own no rows of the last, half block (N-tile 8k + w)
+  const bool half_idle = TG::HALF && __builtin_amdgcn_readfirstlane(w) >= 4;
 #pragma unroll
   for (int s = 0; s < O::KSTEPS; ++s) {
 #pragma unroll
     for (int k = 0; k < NBK; ++k) {
+      if (k == NBK - 1 && half_idle) continue;
       const typename O::B b = O::load_b(tl.lds, TG::row(128 * k + 16 * w + c16 + s - (WALK ? 2 : 1)), s, q);
       acc[k] = O::mma(a.v[0][s], b, acc[k], a.sc[0], s);
     }

@@ -15,12 +15,13 @@
 
 namespace hybw {
 namespace PP = h16xw;
-constexpr int WNBK = 4;
+constexpr int WNBK = (RDN_WALK_ROWS_MIX + 127) / 128;    // in-place blocks (the last may be half)
 using WG = WalkGeo<WNBK>;
 static_assert(PP::WT == WG::WB && PP::CG == WG::GRD, "one walk tile, two engines");
 constexpr int RIGHT_C0 = walk_shift(RRCDNET) - 16;   // the right stem's extra shift (both heads at 28)
 constexpr int CARRY_BYTES = 9 * 2 * 128 + 6 * 2 * 256 + 52 * 128;   // layers 0-8 | 9-14 | left 15-28
 static_assert(PP::CARRY_OFF + CARRY_BYTES <= 163840 - 64, "carry slots below the vote words");
+static_assert(WG::LDS <= PP::CARRY_OFF, "the in-place tile inside the ping-pong buffers");
 
 // layer 9's outputs, split in VGPRs into the in-place tile's planes (rrcdnet_hybrid.hpp H8Stage on the
 // walk rows: r0 includes the carry rows in front)
@@ -69,9 +70,13 @@ __device__ __forceinline__ void stage_carry(char* lds, const PP::Tile& t) {
   }
 }
 
+// Diagnostic builds (tools/hyb_stamps.py with RDN_WALK=1, -DRDN_HYB_STAMPS=1): phase stamps summed over
+// each spectrum's tiles (hyb640::HybStamps, flushed once per spectrum); nothing in the product build
+using Stamps = hyb640::HybStamps;
+
 template <bool EDGE>
 __device__ __forceinline__ void tile(Tile& tl, PP::Tile& t16, float* y, int t, int ntiles, PP::Frags& F0, PP::Frags& F1,
-                                     PP::StemX& xs, unsigned* status) {
+                                     PP::StemX& xs, unsigned* status, Stamps& st) {
   constexpr int TAIL = F16MIX_TAIL, PPL = 14 - TAIL;      // 9 plain right layers, layer 9 staged
   static_assert(PPL % 2 == 1, "the staged layer reads BUF1");
   using HO = HeadOut<MODE_H8, WNBK>;
@@ -83,11 +88,13 @@ __device__ __forceinline__ void tile(Tile& tl, PP::Tile& t16, float* y, int t, i
   PP::stem(t16, 0, PP::BUF0, xs);
   F0 = F1;
   PP::lds_barrier();
+  st(0);
   for (int i = 0; i < PPL / 2; ++i) {
     PP::layer<PP::RELU, EDGE>(t16, PP::BUF0, PP::BUF1, 1, F0, F1);
     PP::layer<PP::RELU, EDGE>(t16, PP::BUF1, PP::BUF0, 1, F1, F0);
   }
   PP::layer<PP::RELU, EDGE>(t16, PP::BUF0, PP::BUF1, 1, F0, F1);
+  st(1);
   {
     H8Stage stg;
     PP::layer<PP::STAGE, EDGE>(t16, PP::BUF1, PP::BUF0, 1, F1, F0, false, nullptr, nullptr, &stg);
@@ -105,12 +112,15 @@ __device__ __forceinline__ void tile(Tile& tl, PP::Tile& t16, float* y, int t, i
   tl.first = t16.first;
   tl.layer = PPL + 1;
   lds_barrier();
+  st(2);
   const uint8_t* rhead = tl.big + (size_t)F16MIX_RHEAD_REC * BIG_BYTES_H8;
   for (int i = 0; i < TAIL; ++i)
     conv<MODE_H8, RELU, 1, EDGE, WNBK, true, true, true, true>(tl, 1, id, a, true, i + 1 < TAIL ? nullptr : rhead);
+  st(3);
   const PP::StemX xl = PP::walk_stem_load(t16, t, 0);
   float rk[HO::ROWS];
   head_h8_mfma<WNBK, true>(tl, a, rk);
+  st(4);
   // left branch: layers 15-28 and the head on the ping-pong engine
   t16.cs_cur = tl.cs_cur;
   t16.dn_prev = 0;                      // the stem recomputes its carry rows
@@ -120,12 +130,14 @@ __device__ __forceinline__ void tile(Tile& tl, PP::Tile& t16, float* y, int t, i
   PP::lds_barrier();                    // the left stem overwrites the rows the right head read
   PP::stem(t16, 1, PP::BUF0, xl);
   PP::lds_barrier();
+  st(5);
   for (int i = 0; i < 7; ++i) {        // left layer j has d = 1 at j = 7, else 2; the head reads with d = 1
     t16.dnext = 2 * i + 1 == 7 ? 1 : 2;
     PP::layer<PP::RELU, EDGE>(t16, PP::BUF0, PP::BUF1, 2, F0, F1);
     t16.dnext = i == 6 ? 1 : 2;
     PP::layer<PP::RELU, EDGE>(t16, PP::BUF1, PP::BUF0, 2 * i + 1 == 7 ? 1 : 2, F1, F0);
   }
+  st(6);
   float xv[HO::ROWS];
 #pragma unroll
   for (int k = 0; k < HO::ROWS; ++k) {  // the combine's x, fetched before the left head
@@ -137,6 +149,7 @@ __device__ __forceinline__ void tile(Tile& tl, PP::Tile& t16, float* y, int t, i
   xs = PP::walk_stem_load(t16, t + 1, RIGHT_C0);
   float l[PP::HN];
   PP::head<EDGE>(t16, PP::BUF0, F0, F1, true, l, 0);
+  st(7);
   // the left head's rows to the right head's lanes through LDS (BUF1, unread since layer 28's
   // barrier); the tail's range vote rides on the same barrier
   float* lrow = (float*)(tl.lds + PP::BUF1);
@@ -153,16 +166,17 @@ __device__ __forceinline__ void tile(Tile& tl, PP::Tile& t16, float* y, int t, i
   float o[HO::ROWS];
 #pragma unroll
   for (int k = 0; k < HO::ROWS; ++k)        // x - (r + l)/2, one rounding
-    o[k] = (float)((double)xv[k] - ((double)rk[k] + (double)lrow[PP::CG + HO::row(k)]) * 0.5);
+    o[k] = (float)((double)xv[k] - ((double)rk[k] + (double)lrow[min(PP::CG + HO::row(k), PP::WB - 1)]) * 0.5);
   if (sat) nan_rows(o);
   if (HO::writer()) {
 #pragma unroll
     for (int k = 0; k < HO::ROWS; ++k) {
       const int p = tl.base + HO::row(k);
-      if (in_range(p, L)) y[p] = o[k];
+      if (HO::row(k) < WG::WB && in_range(p, L)) y[p] = o[k];
     }
   }
   PP::lds_barrier();                    // the next tile's stem and layers overwrite BUF0 / BUF1
+  st(8);
 }
 
 }  // namespace hybw

@@ -15,12 +15,12 @@ if [[ " $STAGES " == *" bench "* ]]; then
   grep "^{" $OUT/bench.log | tail -1 > $OUT/bench.json
 fi
 if [[ " $STAGES " == *" kt "* ]]; then
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py --no-cpu-baseline --no-configs > $OUT/kt_bench.log 2>&1
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py --no-cpu-baseline --no-configs --sustained-seconds 0 > $OUT/kt_bench.log 2>&1
   rc=$?; echo "kt rc=$rc"; tail -1 $OUT/kt_bench.log | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi
   grep "^{" $OUT/kt_bench.log | tail -1 > $OUT/kt_bench.json
 fi
 # PMC: the timed launches only (no batch-1 loop, variants, pipeline or configs)
-SHORT="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-variants --no-pipeline --no-batch1 --no-configs"
+SHORT="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-variants --no-pipeline --no-batch1 --no-configs --sustained-seconds 0"
 if [[ " $STAGES " == *" pmc "* ]]; then
   for spec in ${PROFILE_SPECS:-RRCDNet:f16:8192 RRCDNet:f16-plain:8192 ADSDN:f16:2048 APIDN:f16:2048}; do
     IFS=: read -r arch dt bsz <<< "$spec"

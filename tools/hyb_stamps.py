@@ -17,6 +17,13 @@ PHASES = ["right stem", "window vote", "right ping-pong layers 0-7", "layers 8, 
           "in-place corrected tail (5)", "right head (MFMA)", "left layer-0 operands + barrier", "left stem",
           "left layers 15-28 (14)", "left head + vote + combine + store"]
 PER_LAYER = {2: 8, 4: 5, 8: 14}
+# RDN_WALK=1: the RDN_F16MIX walk kernel (rrcdnet_hybrid_walk.hpp), stamps summed over a spectrum's tiles
+WALK_PHASES = ["right stem + barrier", "right ping-pong layers 0-8 (9)", "layer 9 staged + planes + tail operands",
+               "in-place corrected tail (5)", "right head (MFMA)", "left operands + stem + barriers",
+               "left layers 15-28 (14)", "left head", "vote + combine + store + barrier", "-"]
+WALK_PER_LAYER = {1: 9, 3: 5, 6: 14}
+if os.environ.get("RDN_WALK") == "1":
+    PHASES, PER_LAYER = WALK_PHASES, WALK_PER_LAYER
 
 
 def main():
@@ -28,7 +35,9 @@ def main():
             getattr(lib, fn).argtypes, getattr(lib, fn).restype = args, res
     dev = torch.device("cuda")
     B, L = 2048, 10000
-    _, noisy, _, _ = engine.generate(B, 1, signal_length=L, device=dev)
+    # no spikes: every spectrum takes the walk (a spiked one would stamp the tiled phases into the sums)
+    _, noisy, _, _ = engine.generate(B, 1, signal_length=L, device=dev,
+                                     extreme_noise_prob=0.0 if os.environ.get("RDN_WALK") == "1" else 0.05)
     torch.manual_seed(0)
     model = R.RRCDNet()
     names = engine.param_names("RRCDNet")
@@ -57,8 +66,10 @@ def main():
     w = ws.view(torch.int64).cpu().tolist()
     n = w[1 + len(PHASES)]
     tot = sum(w[1:1 + len(PHASES)])
+    tiles = -(-(L + 28) // 512) if os.environ.get("RDN_WALK") == "1" else 1
     print(f"{e0.elapsed_time(e1) / 5:.2f} ms per forward of {B} spectra; {n} hybrid workgroups stamped; "
-          f"{tot / n:.0f} cycles per workgroup")
+          f"{tot / n:.0f} cycles per workgroup ({tiles} tiles each; per tile below)")
+    n *= tiles
     for k, name in enumerate(PHASES):
         c = w[1 + k] / n
         extra = f"  ({c / PER_LAYER[k]:.0f} per layer)" if k in PER_LAYER else ""
