@@ -405,11 +405,10 @@ struct BAddr {
 
 // steps between two of the next layer's operand loads: 4 on the 640-row tile (16x16x32: 3 is
 // -0.5 %, 2 is -2 %), as many as fit otherwise
-#ifdef RDN_H16_LDSTEP
-constexpr int LDSTEP = RDN_H16_LDSTEP;
-#else
-constexpr int LDSTEP = (KS * NT - 1) / (NLOAD - 1) < 4 ? (KS * NT - 1) / (NLOAD - 1) : 4;
+#ifndef RDN_H16_LDSTEP
+#define RDN_H16_LDSTEP 4
 #endif
+constexpr int LDSTEP = (KS * NT - 1) / (NLOAD - 1) < RDN_H16_LDSTEP ? (KS * NT - 1) / (NLOAD - 1) : RDN_H16_LDSTEP;
 static_assert(LDSTEP >= 1 && LDSTEP * (NLOAD - 1) < KS * NT, "every operand load of the next layer must be issued");
 
 // One Conv1d(64, 64, 3, dilation=dil, padding=dil) over the tile, src -> dst: this wave's 32

@@ -248,7 +248,7 @@ class Workspace:
                                                  ctypes.c_void_p(self.stream.cuda_stream)), "rdn_forward_status")
 
 
-def forward(arch, dtype, packed, x, out=None, check=True, workspace=None):
+def forward(arch, dtype, packed, x, out=None, check=True, workspace=None, _ws_checked=False):
     """y = Model(x) for x float32 (N, 1, L) (or (N, L)) on the GPU.
 
     ``dtype`` is an engine dtype name or ABI code (resolve_dtype).  The CBAM networks run one
@@ -257,6 +257,7 @@ def forward(arch, dtype, packed, x, out=None, check=True, workspace=None):
     the kernel and raises EngineError if a hand-off timed out, RangeError if a tile saturated
     (rdn_forward_status).  A batched caller passes one ``Workspace`` to every forward with
     ``check=False`` and calls ``workspace.check()`` once at the end (the status words are sticky);
+    (``_ws_checked``: the caller has just verified ``workspace.fits`` for this input.)
     ``check=False`` without a workspace keeps the launch asynchronous and unchecked (benchmarks: the
     affected outputs are NaN).  On the CBAM networks (ADSDN / APIDN) a saturated tile is NaN, but its
     clamped CBAM statistics have already reached the other tiles of its spectrum through the team
@@ -279,7 +280,7 @@ def forward(arch, dtype, packed, x, out=None, check=True, workspace=None):
     ws = workspace
     if ws is None and (a in CBAM_IDS or (check and code in RANGE_CODES)):
         ws = Workspace(a, code, n, L, x.device)
-    elif ws is not None and not ws.fits(a, code, n, L, x.device):
+    elif ws is not None and not _ws_checked and not ws.fits(a, code, n, L, x.device):
         raise ValueError("workspace was made for another network, dtype, length, device, stream or a smaller batch")
     L_ = _lib.lib()
     _lib.check(L_.rdn_forward(a, code, ctypes.c_void_p(packed.data_ptr()), ctypes.c_void_p(x.data_ptr()),

@@ -275,6 +275,27 @@ def test_packing_cache_tracks_weight_updates():
     assert np.allclose(y1 - y0, 1.0, atol=1e-5)
 
 
+@pytest.mark.parametrize("arch,dtype", [("DenoiseCNN", "f16"), ("RRCDNet", "f16")])
+def test_speculative_launch_tracks_weight_updates(arch, dtype):
+    """The 16-bit fused forwards launch with the cached blob and check the pack cache after the launch
+    (models._EngineNet.forward): an in-place weight update and a storage swap between calls are still
+    seen -- the batch is re-launched with a fresh blob (head bias + 1: the output moves by exactly 1 on
+    1DCNN, by -1/2 on RRCDNet, whose output is x - (r + l)/2)."""
+    m = _model(arch, "synth", dtype)
+    head = m.layers[20] if arch == "DenoiseCNN" else m.right_net[18]
+    step = 1.0 if arch == "DenoiseCNN" else -0.5
+    x = np.random.default_rng(2).uniform(0, 1, (2, 1500)).astype(np.float32)
+    y0 = _run(m, x)
+    assert np.array_equal(_run(m, x), y0)                     # cached blob, unchanged weights
+    with torch.no_grad():
+        head.bias.add_(1.0)                                   # in place: the version counter moves
+    y1 = _run(m, x)
+    assert np.allclose(y1 - y0, step, atol=1e-4), float(np.abs(y1 - y0 - step).max())
+    head.bias.data = head.bias.data + 1.0                     # storage swap: the data pointer moves
+    y2 = _run(m, x)
+    assert np.allclose(y2 - y1, step, atol=1e-4), float(np.abs(y2 - y1 - step).max())
+
+
 def test_rejects_unsupported_use():
     import raman_mi355x as R
     m = R.RRCDNet().cuda().eval()

@@ -19,7 +19,7 @@ VARIANTS = {"base": "", "prev": "", "cur": "", "cur2": "", "nolds": "-DRDN_ABLAT
             "nomfma": "-DRDN_ABLATE_NOMFMA", "nostore": "-DRDN_ABLATE_NOSTORE", "noaload": "-DRDN_ABLATE_NOALOAD",
             "pf3": "-DRDN_H16_PF=3", "ieee": "", "stamps": "-DRDN_TEAM_STAMPS=1", "nobar": "-DRDN_ABLATE_NOBARRIER", "dsdn3": "-DRDN_DSDN_NBK=3", "comp0": "-DRDN_F32_COMP=0",
             "chunk1": "-DRDN_F32_CHUNK=1", "chunk3": "-DRDN_F32_CHUNK=3", "chunk4": "-DRDN_F32_CHUNK=4",
-            "h16f16": "-DRDN_H16_F16=1", "ld2": "-DRDN_H16_LDSTEP=2", "ld4": "-DRDN_H16_LDSTEP=4", "pf2": "-DRDN_H16_PF=2", "pf4": "-DRDN_H16_PF=4", "alledge": "-DRDN_ABLATE_ALLEDGE -DRDN_TEAM_STAMPS=1",
+            "h16f16": "-DRDN_H16_F16=1", "ld2": "-DRDN_H16_LDSTEP=2", "ld3": "-DRDN_H16_LDSTEP=3", "ld4": "-DRDN_H16_LDSTEP=4", "pf2": "-DRDN_H16_PF=2", "pf4": "-DRDN_H16_PF=4", "alledge": "-DRDN_ABLATE_ALLEDGE -DRDN_TEAM_STAMPS=1",
             "tail3": "-DRDN_F16MIX_TAIL=3", "tail4": "-DRDN_F16MIX_TAIL=4", "tail5": "-DRDN_F16MIX_TAIL=5", "nowin": "-DRDN_F16MIX_WIN=0", "nostem": "-DRDN_ABLATE_NOSTEM",
             "tail0": "-DRDN_F16MIX_TAIL=0", "tail2": "-DRDN_F16MIX_TAIL=2", "hybstamps": "-DRDN_HYB_STAMPS=1",
             "w512": "-DRDN_WALK_ROWS=512", "w448": "-DRDN_WALK_ROWS=448", "mix512": "-DRDN_WALK_ROWS_MIX=512", "mhead": "", "lbar": "", "stg": "", "vote": "", "comb": "", "track": "", "trk2": "", "sdpp": "", "cur": "", "resplain": ""}
