@@ -145,7 +145,9 @@ constexpr int H16_WALK_ROWS = RDN_WALK_ROWS;
 #ifndef RDN_WALK_ROWS_MIX
 #define RDN_WALK_ROWS_MIX 576
 #endif
-__host__ __device__ constexpr int walk_shift(int arch) { return arch == DENOISECNN ? 19 : arch == RRCDNET ? 28 : 0; }
+__host__ __device__ constexpr int walk_shift(int arch) {
+  return arch == DENOISECNN ? 19 : arch == RRCDNET ? 28 : arch == PIDN ? 31 : 0;
+}
 
 // receptive half-width (rows of halo needed on each side of a tile's outputs)
 __host__ __device__ constexpr int fused_halo(int arch) {

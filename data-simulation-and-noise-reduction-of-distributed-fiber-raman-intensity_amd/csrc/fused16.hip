@@ -237,6 +237,33 @@ __device__ __forceinline__ void rrcdnet_tile(Tile& tl, float* y, int t, int ntil
   lds_barrier();
 }
 
+// PIDN/train.py:101-106 — h = relu(stem x); 15 x [conv+BN+ReLU, conv+BN]; sigmoid(conv_out(y + h)):
+// head at shift 31.  The identity h is recomputed from x at the last layer's shift (stem<true>), on the
+// computed rows only: the carry rows in front already hold the previous tile's y + h (layer_carry
+// saved them after its stem<true>)
+constexpr int PIDN_SHIFT = walk_shift(PIDN);
+static_assert(PIDN_SHIFT == 30 + 1, "30 layers and the head, d = 1");
+template <bool EDGE>
+__device__ __forceinline__ void pidn_tile(Tile& tl, float* y, int t, int ntiles, Frags& F0, Frags& F1, StemX& xs) {
+  walk_start(tl, t, 0);
+  stem(tl, 0, BUF0, xs);
+  F0 = F1;
+  lds_barrier();
+  for (int b = 0; b < 15; ++b) {
+    layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F0, F1);
+    layer<LINEAR, EDGE>(tl, BUF1, BUF0, 1, F1, F0);
+  }
+  stem<true>(tl, 0, BUF0);            // + identity, at this shift (stem_load reads x at tl.base)
+  lds_barrier();
+  xs = walk_stem_load(tl, t + 1, 0);
+  float o[HN];
+  head<EDGE>(tl, BUF0, F0, F1, true, o, 0);
+#pragma unroll
+  for (int k = 0; k < HN; ++k) o[k] = 1.0f / (1.0f + expf(-o[k]));
+  store_out_walk(tl, y, o);
+  lds_barrier();
+}
+
 #define H16_WALK_KERNEL(name, SHIFT, C0)                                                                   \
   __global__ __launch_bounds__(THREADS) void name##_walk(const uint8_t* __restrict__ blob,                 \
                                                          const float* __restrict__ x, float* __restrict__ y, \
@@ -258,6 +285,7 @@ __device__ __forceinline__ void rrcdnet_tile(Tile& tl, float* y, int t, int ntil
 
 H16_WALK_KERNEL(denoisecnn, DENOISECNN_SHIFT, 0)
 H16_WALK_KERNEL(rrcdnet, RRCDNET_SHIFT, RRCDNET_RIGHT_C0)
+H16_WALK_KERNEL(pidn, PIDN_SHIFT, 0)
 
 }  // namespace H16_NS
 
@@ -272,6 +300,7 @@ hipError_t H16_LAUNCH(int arch, const uint8_t* blob, const float* x, float* y, i
   switch (arch) {
     case DENOISECNN: k = H16_NS::denoisecnn_walk; shift = H16_NS::DENOISECNN_SHIFT; break;
     case RRCDNET: k = H16_NS::rrcdnet_walk; shift = H16_NS::RRCDNET_SHIFT; break;
+    case PIDN: k = H16_NS::pidn_walk; shift = H16_NS::PIDN_SHIFT; break;
     default: return hipErrorInvalidValue;
   }
   const hipError_t e = ensure_dynamic_lds((const void*)k, H16_ATTR_SLOT0 + arch, (int)H16_NS::LDS_BYTES, stream_device(stream));
