@@ -146,7 +146,7 @@ constexpr int H16_WALK_ROWS = RDN_WALK_ROWS;
 #define RDN_WALK_ROWS_MIX 576
 #endif
 __host__ __device__ constexpr int walk_shift(int arch) {
-  return arch == DENOISECNN ? 19 : arch == RRCDNET ? 28 : arch == PIDN ? 31 : 0;
+  return arch == DENOISECNN ? 19 : arch == RRCDNET ? 28 : arch == PIDN ? 31 : arch == DSDN ? 33 : 0;
 }
 
 // receptive half-width (rows of halo needed on each side of a tile's outputs)

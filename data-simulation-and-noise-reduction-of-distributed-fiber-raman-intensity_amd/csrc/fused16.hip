@@ -264,6 +264,31 @@ __device__ __forceinline__ void pidn_tile(Tile& tl, float* y, int t, int ntiles,
   lds_barrier();
 }
 
+// DSDN/train.py:120-126 — relu(relu(stem)), relu(conv1), relu(conv2), 15 ResNet blocks, conv_out:
+// head at shift 33.  Each block's second conv adds the block input two rows up (fused16.hpp layer,
+// walk RES_RELU); the block's first conv hands it the identity of its first N-tile (walk_id).
+constexpr int DSDN_SHIFT = walk_shift(DSDN);
+static_assert(DSDN_SHIFT == 32 + 1, "32 layers and the head, d = 1");
+template <bool EDGE>
+__device__ __forceinline__ void dsdn_tile(Tile& tl, float* y, int t, int ntiles, Frags& F0, Frags& F1, StemX& xs) {
+  walk_start(tl, t, 0);
+  stem(tl, 0, BUF0, xs);
+  F0 = F1;
+  lds_barrier();
+  layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F0, F1);           // conv1
+  layer<RELU, EDGE>(tl, BUF1, BUF0, 1, F1, F0);           // conv2
+  for (int b = 0; b < 15; ++b) {                           // x in BUF0 is the block identity
+    V id0;
+    layer<RELU, EDGE>(tl, BUF0, BUF1, 1, F0, F1, true, nullptr, nullptr, (NoStage*)nullptr, &id0);
+    layer<RES_RELU, EDGE>(tl, BUF1, BUF0, 1, F1, F0, true, nullptr, nullptr, (NoStage*)nullptr, &id0);
+  }
+  xs = walk_stem_load(tl, t + 1, 0);
+  float o[HN];
+  head<EDGE>(tl, BUF0, F0, F1, true, o, 0);
+  store_out_walk(tl, y, o);
+  lds_barrier();
+}
+
 #define H16_WALK_KERNEL(name, SHIFT, C0)                                                                   \
   __global__ __launch_bounds__(THREADS) void name##_walk(const uint8_t* __restrict__ blob,                 \
                                                          const float* __restrict__ x, float* __restrict__ y, \
@@ -286,6 +311,7 @@ __device__ __forceinline__ void pidn_tile(Tile& tl, float* y, int t, int ntiles,
 H16_WALK_KERNEL(denoisecnn, DENOISECNN_SHIFT, 0)
 H16_WALK_KERNEL(rrcdnet, RRCDNET_SHIFT, RRCDNET_RIGHT_C0)
 H16_WALK_KERNEL(pidn, PIDN_SHIFT, 0)
+H16_WALK_KERNEL(dsdn, DSDN_SHIFT, 0)
 
 }  // namespace H16_NS
 
@@ -301,6 +327,7 @@ hipError_t H16_LAUNCH(int arch, const uint8_t* blob, const float* x, float* y, i
     case DENOISECNN: k = H16_NS::denoisecnn_walk; shift = H16_NS::DENOISECNN_SHIFT; break;
     case RRCDNET: k = H16_NS::rrcdnet_walk; shift = H16_NS::RRCDNET_SHIFT; break;
     case PIDN: k = H16_NS::pidn_walk; shift = H16_NS::PIDN_SHIFT; break;
+    case DSDN: k = H16_NS::dsdn_walk; shift = H16_NS::DSDN_SHIFT; break;
     default: return hipErrorInvalidValue;
   }
   const hipError_t e = ensure_dynamic_lds((const void*)k, H16_ATTR_SLOT0 + arch, (int)H16_NS::LDS_BYTES, stream_device(stream));

@@ -475,7 +475,7 @@ struct NoStage {
 template <int EPI, bool EDGE, class SG = NoStage>
 __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int dil, const Frags& F, Frags& G,
                                       bool has_next = true, V* idv = nullptr, ChanStats* cs = nullptr,
-                                      SG* stg = nullptr) {
+                                      SG* stg = nullptr, V* walk_id = nullptr) {
   const int lane = tid() & 63, w = __builtin_amdgcn_readfirstlane(tid() >> 6), h = w / RB;
   const int next = tl.layer + 1;
   asm volatile("" : "+s"(src), "+s"(dst));   // per-layer addresses: not hoisted out of a network's loop (spills)
@@ -502,6 +502,7 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   if (EDGE && pos0 >= tl.L + (WALK ? 0 : 2)) {
     if constexpr (WALK) carry_store(tl, dst, CA, cc, CROW);
     if constexpr (EPI != STAGE) zero_outside(tl, dst, pos0 - tl.base, h, lane);
+    if (WALK && walk_id) *walk_id = *(const V*)(tl.lds + src + (h ? tl.koff[2][1] : tl.koff[2][0]));
     if (has_next) load_frags(tl, next, G);
     if constexpr (EPI == LINEAR_SAVE) {
 #pragma unroll
@@ -514,8 +515,19 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   const LaneOff lo = lane_off();
 
   // bias (+ identity), ReLU, zero rows outside [0, L), round, store 8 channels as one 16-B slot
-  auto store_slot = [&](V* p, f32x8 v, bool valid) {
-    if (EPI == RES_RELU) v += __builtin_convertvector(*p, f32x8);
+  // Walk RES_RELU (DSDN's second block conv, in place over the block input): the identity of output
+  // row r is block-input row r - 2 (the input is two layers less shifted), which the epilogue of the
+  // N-tile before may already have overwritten: each N-tile's identity is read at its first k-step,
+  // ahead of that epilogue in this wave's LDS order, and N-tile 0's -- two rows of the previous row
+  // block, or the carry rows that layer_carry (a) rewrites -- by the layer before, ahead of its
+  // closing barrier (walk_id)
+  V idn[2];
+  const int sid = (int)dst + (h ? tl.koff[2][1] : tl.koff[2][0]);   // walk: row r0 - 2 of the block input
+  auto store_slot = [&](V* p, f32x8 v, bool valid, int n) {
+    if constexpr (EPI == RES_RELU) {
+      if constexpr (WALK) v += __builtin_convertvector(n == 0 ? *walk_id : idn[n & 1], f32x8);
+      else v += __builtin_convertvector(*p, f32x8);
+    }
 #if RDN_H16_F16
     // ReLU after the rounding, on packed f16 (4 v_pk_max_f16 instead of 8 v_max_f32; the rounding is
     // monotone, so max(f16(v), 0) = f16(max(v, 0)) up to the sign of a zero)
@@ -560,7 +572,7 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
         }
       }
     }
-    store_slot(p, v, valid);
+    store_slot(p, v, valid, n);
   };
 
   Acc prev;
@@ -580,6 +592,9 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
 #else
       if (kp < K) B[kp % (PF + 1)] = *(const V*)(tl.lds + ba.at(kp / KS, kp % KS));
 #endif
+      if constexpr (WALK && EPI == RES_RELU) {
+        if (n > 0 && s == 0) idn[n & 1] = *(const V*)(tl.lds + sid + n * NR * ROWB);
+      }
       mstep(F, s, B[k % (PF + 1)], acc);
       if (n > 0 && s == 1) epilogue(n - 1, prev);
       if (WALK && n == 1 && s == 0) carry_store(tl, dst, CA, cc, CROW);
@@ -594,6 +609,9 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   }
   epilogue(NT - 1, prev);
   if constexpr (EDGE && EPI != STAGE) zero_outside(tl, dst, pos0 - tl.base, h, lane);
+  // walk: the next layer's (RES_RELU) N-tile-0 identity, rows r0 - 2 of this layer's input (stable
+  // until the barrier below)
+  if (WALK && walk_id) *walk_id = *(const V*)(tl.lds + src + (h ? tl.koff[2][1] : tl.koff[2][0]));
   tl.layer += 1;
 #if defined(RDN_ABLATE_NOBARRIER)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -78,7 +78,7 @@ def test_fp32_matches_reference(arch, which, inputs):
         assert ok, f"{arch}/{which}/{name}: fp32 {msg}"
 
 
-WALK = ["DenoiseCNN", "RRCDNet", "PIDN"]      # networks with a walk kernel (fused16_walk.hip)
+WALK = ["DenoiseCNN", "RRCDNet", "PIDN", "DSDN"]      # networks with a walk kernel (fused16_walk.hip)
 
 
 def _tiles(dtype, monkeypatch):
