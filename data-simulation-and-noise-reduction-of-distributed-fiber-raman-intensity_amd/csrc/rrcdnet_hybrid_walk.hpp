@@ -117,7 +117,11 @@ __device__ __forceinline__ void tile(Tile& tl, PP::Tile& t16, float* y, int t, i
   for (int i = 0; i < TAIL; ++i)
     conv<MODE_H8, RELU, 1, EDGE, WNBK, true, true, true, true>(tl, 1, id, a, true, i + 1 < TAIL ? nullptr : rhead);
   st(3);
+  // the left branch's stem inputs and layer-15 operands, fetched before the right head: their latency
+  // hides under its MFMAs (F0 is free since the staged layer)
   const PP::StemX xl = PP::walk_stem_load(t16, t, 0);
+  t16.layer = 15;
+  PP::load_frags(t16, 15, F0);
   float rk[HO::ROWS];
   head_h8_mfma<WNBK, true>(tl, a, rk);
   st(4);
@@ -125,8 +129,6 @@ __device__ __forceinline__ void tile(Tile& tl, PP::Tile& t16, float* y, int t, i
   t16.cs_cur = tl.cs_cur;
   t16.dn_prev = 0;                      // the stem recomputes its carry rows
   t16.base = t * PP::WT - PP::CG;
-  t16.layer = 15;
-  PP::load_frags(t16, 15, F0);
   PP::lds_barrier();                    // the left stem overwrites the rows the right head read
   PP::stem(t16, 1, PP::BUF0, xl);
   PP::lds_barrier();

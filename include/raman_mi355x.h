@@ -77,7 +77,10 @@ typedef enum {
  *              from a packed blob.
  * RDN_F16 / RDN_F16MIX launches that would occupy at most half the CUs with 640-row tiles (e.g. one
  * spectrum per call, evaulate.py:29-32) run on 256-row tiles (same arithmetic and, for RDN_F16MIX, the
- * same hybrid composition); the environment variable RDN_SHORT_TILES=0/1 forces either. */
+ * same hybrid composition); the environment variable RDN_SHORT_TILES=0/1 forces either.  Launches large
+ * enough to give every CU several spectra run RDN_F16 (DenoiseCNN, RRCDNet, DSDN, PIDN) and RDN_F16MIX
+ * on the walk geometry instead: one workgroup walks a whole spectrum with time-skewed layers and no
+ * halo recompute (same per-output arithmetic; RDN_WALK=0/1 forces either). */
 typedef enum { RDN_F32 = 0, RDN_BF16 = 1, RDN_BF16X3 = 2, RDN_F16F8 = 3, RDN_F16 = 4, RDN_F16MIX = 5 } rdn_dtype;
 
 enum {
