@@ -19,8 +19,11 @@ if [[ " $STAGES " == *" parity "* ]]; then
   timeout -k 10 300 python -u tools/parity_report.py --out $OUT/parity.md > $OUT/parity.log 2>&1
   rc=$?; tail -2 $OUT/parity.md; if [ $rc -ne 0 ]; then exit $rc; fi
 fi
-STAGES="$(echo " $STAGES " | grep -o ' bench \| kt \| pmc ' | tr -d '\n')" bash scripts/gpu_final.sh
-rc=$?; if [ $rc -ne 0 ]; then exit $rc; fi
+INNER="$(echo " $STAGES " | grep -o ' bench \| kt \| pmc ' | tr -d '\n')"
+if [ -n "$INNER" ]; then
+  STAGES="$INNER" bash scripts/gpu_final.sh
+  rc=$?; if [ $rc -ne 0 ]; then exit $rc; fi
+fi
 if [[ " $STAGES " == *" throughput "* ]]; then
   timeout -k 10 400 python -u tools/throughput_table.py --out $OUT/throughput.md > $OUT/throughput.log 2>&1
   rc=$?; tail -3 $OUT/throughput.log; exit $rc

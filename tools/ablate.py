@@ -199,5 +199,71 @@ def parity():
                       f"(ref vs f64 {worst[2]:.2e})", flush=True)
 
 
+def scaled():
+    """fp32 on scaled inputs (tests/test_range_gpu.py's cases): per built variant, network and scale, the
+    engine's max distance from the float64 forward over the reference fp32's own distance (the test's
+    factor):  python tools/ablate.py scaled [archs...]"""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "data-simulation-and-noise-reduction-of-distributed-fiber-raman-intensity_amd"))
+    from conftest import golden_inputs, golden_state_dict
+    import raman_mi355x as R
+    from raman_mi355x import _lib, engine
+    dev = torch.device("cuda")
+    archs = sys.argv[2:] or ["DenoiseCNN", "RRCDNet", "DSDN", "PIDN", "ADSDN", "APIDN"]
+    inp = golden_inputs()
+    xs = [inp["main_noisy"][:2], inp["edge1000_noisy"]]
+    libs = {}
+    for name in VARIANTS:
+        path = os.path.join(OUT, f"lib_{name}.so")
+        if os.path.exists(path):
+            lib = ctypes.CDLL(path)
+            for fn, (args, res) in _lib._SIGNATURES.items():
+                if hasattr(lib, fn):
+                    getattr(lib, fn).argtypes = args
+                    getattr(lib, fn).restype = res
+            libs[name] = lib
+    for arch in archs:
+        sd = golden_state_dict(arch, "trained")
+        m32, m64 = R.MODELS[arch](), R.MODELS[arch]()
+        m32.load_state_dict(sd, strict=True)
+        m64.load_state_dict(sd, strict=True)
+        m32, m64 = m32.eval(), m64.double().eval()
+        aid, code = engine._arch(arch), engine.resolve_dtype(arch, "fp32")
+        names = engine.param_names(arch)
+        host = [sd[k].detach().float().contiguous() for k in names]
+        ptrs = (ctypes.c_void_p * len(host))(*[t.data_ptr() for t in host])
+        numels = (ctypes.c_int64 * len(host))(*[t.numel() for t in host])
+        for scale in [1.0, 10.0, 100.0, 1000.0]:
+            refs = []
+            for x in xs:
+                xt = torch.from_numpy((x * scale).astype(np.float32)).unsqueeze(1)
+                with torch.no_grad():
+                    refs.append((xt, m32(xt).squeeze(1).numpy(), m64(xt.double()).squeeze(1).numpy()))
+            line = []
+            for name, lib in libs.items():
+                size = ctypes.c_size_t()
+                assert lib.rdn_packed_size(aid, code, ctypes.byref(size)) == 0
+                blob = torch.empty(size.value, dtype=torch.uint8)
+                assert lib.rdn_pack(aid, code, ptrs, numels, len(host), ctypes.c_void_p(blob.data_ptr()), size.value) == 0
+                blob = blob.to(dev)
+                worst_e, worst_r = 0.0, 0.0
+                for xt, r32, y64 in refs:
+                    xd = xt.to(dev)
+                    y = torch.empty_like(xd)
+                    wsz = ctypes.c_size_t()
+                    lib.rdn_workspace_size(aid, code, xd.shape[0], xd.shape[-1], ctypes.byref(wsz), None)
+                    ws = torch.empty(max(1, wsz.value), dtype=torch.uint8, device=dev)
+                    rc = lib.rdn_forward(aid, code, blob.data_ptr(), xd.data_ptr(), y.data_ptr(), xd.shape[0], xd.shape[-1],
+                                         ws.data_ptr(), wsz.value, torch.cuda.current_stream().cuda_stream)
+                    assert rc == 0, lib.rdn_last_error()
+                    yh = y.squeeze(1).cpu().numpy()
+                    worst_e = max(worst_e, float(np.abs(yh - y64).max()))
+                    worst_r = max(worst_r, float(np.abs(r32 - y64).max()))
+                line.append(f"{name} {worst_e:.2e} ({worst_e / max(worst_r, 1e-30):.2f}x)")
+            print(f"{arch:10s} x{scale:<6g} ref32-vs-f64 {worst_r:.2e} | " + " | ".join(line), flush=True)
+
+
 if __name__ == "__main__":
-    {"build": build, "run": run, "parity": parity}[sys.argv[1]]()
+    {"build": build, "run": run, "parity": parity, "scaled": scaled}[sys.argv[1]]()
