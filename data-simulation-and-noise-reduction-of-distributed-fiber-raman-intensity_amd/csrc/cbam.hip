@@ -247,7 +247,7 @@ template <int MODE>
 __global__ __launch_bounds__(THREADS) void segment(const uint8_t* __restrict__ blob, const float* __restrict__ x,
                                                    float* __restrict__ y, int L, int T, int tiles, Seg sg) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  using G = Geo<MODE, true>;
+  using G = CbamGeo<MODE>;
   int n;
   Tile tl = make_tile(lds, blob, x, L, T, tiles, sg.halo, n);
   tl.layer = sg.layer0;
@@ -761,7 +761,7 @@ template <int MODE, bool ADS>
 __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restrict__ blob, const float* __restrict__ x,
                                                         float* __restrict__ y, int L, TeamArgs ta) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  using G = Geo<MODE, true>;
+  using G = CbamGeo<MODE>;
   const int team = __builtin_amdgcn_workgroup_id_x() / ta.TT, tile = __builtin_amdgcn_workgroup_id_x() - team * ta.TT;
   const __amdgpu_buffer_rsrc_t hs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(ta.hsave + (size_t)__builtin_amdgcn_workgroup_id_x() * WB * 64 * 4), 0, WB * 64 * 4, 0x00020000);

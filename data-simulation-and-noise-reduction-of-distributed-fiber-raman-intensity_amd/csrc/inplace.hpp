@@ -730,8 +730,9 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   // bf16 modes start the accumulators at the folded bias; exact fp32 keeps the reference's
   // order (sum of products, then + bias) for its 1e-5 parity
   constexpr bool BIAS_INIT = MODE != MODE_F32;
-  constexpr bool COMP = MODE == MODE_F32 && RDN_F32_COMP && S == 0;   // S = 0: compensated chunks (two_sum)
-  constexpr int CH = RDN_F32_CHUNK;
+  // S <= 0: one compensated chain (two_sum) of -S k-step chunks (S = 0: RDN_F32_CHUNK)
+  constexpr bool COMP = MODE == MODE_F32 && RDN_F32_COMP && S <= 0;
+  constexpr int CH = S == 0 ? RDN_F32_CHUNK : -S;
   constexpr int SP = COMP ? 1 : S;                           // MFMA accumulator sets
   f32x4 bias_l[MT];
   uint32_t sc_l[MT];
@@ -827,44 +828,46 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   // MODE_H8: both M-tiles of N-tile i in one write-back, 16-B f16 slot + two 8-B e4m3 slots (3
   // stores instead of 6); ReLU folded into the saturating med3
   auto store_pair = [&](int j, int i) {
-    const int rb = BR * j + (BR / 4) * nq;
-    const bool inside = !EDGE || (tl.base + rb >= 0 && tl.base + rb + BR / 4 <= tl.L);
-    const bool zero = !inside && !in_range(tl.base + rb + 16 * i + c16, tl.L);
-    if (!cout) {                 // plain f16 output (the next layer is uncorrected): no e4m3 planes
-      f16x4 hv[MT];
-#pragma unroll
+    if constexpr (MODE == MODE_H8) {                // (instantiated in every mode, called in MODE_H8)
+      const int rb = BR * j + (BR / 4) * nq;
+      const bool inside = !EDGE || (tl.base + rb >= 0 && tl.base + rb + BR / 4 <= tl.L);
+      const bool zero = !inside && !in_range(tl.base + rb + 16 * i + c16, tl.L);
+      if (!cout) {                 // plain f16 output (the next layer is uncorrected): no e4m3 planes
+        f16x4 hv[MT];
+  #pragma unroll
+        for (int mm = 0; mm < MT; ++mm) {
+          f32x4 v = res[j][i][mm];
+          if (EPI & ADD_ID) v += id[(j * NT + i) * MT + mm];
+          if (EPI & RELU) v = __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
+          if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
+          hv[mm] = __builtin_convertvector(v, f16x4);
+        }
+        *(f16x8*)(tl.lds + sadr[0][0] + (uint32_t)(BR * j + 16 * i) * ROWB_F32) =
+            __builtin_shufflevector(hv[0], hv[1], 0, 1, 2, 3, 4, 5, 6, 7);
+        return;
+      }
+      H8Split x[MT];
+  #pragma unroll
       for (int mm = 0; mm < MT; ++mm) {
         f32x4 v = res[j][i][mm];
         if (EPI & ADD_ID) v += id[(j * NT + i) * MT + mm];
-        if (EPI & RELU) v = __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
-        if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};      // the range guard sees rows in [0, L) only
+        h8_track<(EPI & RELU) != 0>(tl.amax, v);
+        v = (EPI & RELU) ? h8_sat<true>(v) : h8_sat<false>(v);
         if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
-        hv[mm] = __builtin_convertvector(v, f16x4);
+        x[mm] = h8_split(v);
       }
-      *(f16x8*)(tl.lds + sadr[0][0] + (uint32_t)(BR * j + 16 * i) * ROWB_F32) =
-          __builtin_shufflevector(hv[0], hv[1], 0, 1, 2, 3, 4, 5, 6, 7);
-      return;
-    }
-    H8Split x[MT];
-#pragma unroll
-    for (int mm = 0; mm < MT; ++mm) {
-      f32x4 v = res[j][i][mm];
-      if (EPI & ADD_ID) v += id[(j * NT + i) * MT + mm];
-      if (EDGE && zero) v = f32x4{0.f, 0.f, 0.f, 0.f};      // the range guard sees rows in [0, L) only
-      h8_track<(EPI & RELU) != 0>(tl.amax, v);
-      v = (EPI & RELU) ? h8_sat<true>(v) : h8_sat<false>(v);
-      if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
-      x[mm] = h8_split(v);
-    }
-    const uint32_t off = (uint32_t)(BR * j + 16 * i) * ROWB_F32;
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-#if defined(RDN_ABLATE_NOSTORE)
-    if (x[0].hi8 == 0x12345678u)
-#endif
-    {
-      *(f16x8*)(tl.lds + sadr[0][0] + off) = __builtin_shufflevector(x[0].hi, x[1].hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      *(u32x2*)(tl.lds + sadr[0][1] + off) = u32x2{x[0].hi8, x[1].hi8};
-      *(u32x2*)(tl.lds + sadr[0][2] + off) = u32x2{x[0].lo8, x[1].lo8};
+      const uint32_t off = (uint32_t)(BR * j + 16 * i) * ROWB_F32;
+      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  #if defined(RDN_ABLATE_NOSTORE)
+      if (x[0].hi8 == 0x12345678u)
+  #endif
+      {
+        *(f16x8*)(tl.lds + sadr[0][0] + off) = __builtin_shufflevector(x[0].hi, x[1].hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        *(u32x2*)(tl.lds + sadr[0][1] + off) = u32x2{x[0].hi8, x[1].hi8};
+        *(u32x2*)(tl.lds + sadr[0][2] + off) = u32x2{x[0].lo8, x[1].lo8};
+      }
     }
   };
   auto store_block = [&](int j) {
@@ -1064,14 +1067,29 @@ __device__ __forceinline__ void head_h8_mfma(Tile& tl, const LayerA<MODE_H8>& a,
   for (int k = 0; k < NBK; ++k) out[k] = acc[k][0];
 }
 
-// partial sums per accumulator (S = 0: one chain with compensated chunk sums, see two_sum): F32
+// partial sums per accumulator (S <= 0: one chain with compensated chunk sums, see two_sum): F32
 // compensates on the plain stacks (1DCNN, RRCDNet, PIDN; measured on the GPU with RDN_F32_CHUNK = 4:
 // trained RRCDNet 1.25e-5 -> 7.4e-6 vs the fp32 reference, 8.1e-6 -> 4.3e-6 vs float64, -8 %
-// throughput); the residual nets (DSDN, CBAM segments / teams) hold 64 VGPRs of identity and keep
-// one plain chain (compensation spills there: 159 VGPRs in DSDN); split-bf16 / f16f8 error is
-// dominated by the operand split, one chain.
+// throughput).  The residual networks keep one plain chain: DSDN holds 64 VGPRs of identity
+// (compensated it spills 224 B per lane, -11 %), and on the CBAM networks (CbamGeo, RDN_F32_COMP_RES = 1:
+// chunks of RDN_F32_CHUNK_RES k-steps) compensation buys nothing measurable: at inputs x1 - x100 the
+// plain chain is already within 0.65x of the reference fp32's own distance from float64, and at x1000
+// the CBAM gating is chaotic -- the distance is a draw whose size the summation order sets, not its
+// accuracy (APIDN x1000 vs the reference's distance: plain 5.0x, 6-step chunks 1.6x, 4-step 2.0x,
+// 3-step 6.1x, 2-step 1.4x; against the fp32 noise floor of tests/test_range_gpu.py the plain chain is
+// the closest of all, 0.95x) -- for -2.3 % (6-step) to -5 % (4-step) of fp32 throughput
+// (profiles/r05/ablate/fp32_rescomp.log).  Split-bf16 / f16f8 error is dominated by the operand split,
+// one chain.
+#ifndef RDN_F32_COMP_RES
+#define RDN_F32_COMP_RES 0
+#endif
+#ifndef RDN_F32_CHUNK_RES
+#define RDN_F32_CHUNK_RES 4
+#endif
 template <int MODE, bool RES> struct Geo { static constexpr int S = 1; };
 template <> struct Geo<MODE_F32, false> { static constexpr int S = RDN_F32_COMP ? 0 : 2; };
+template <int MODE> struct CbamGeo { static constexpr int S = 1; };
+template <> struct CbamGeo<MODE_F32> { static constexpr int S = RDN_F32_COMP && RDN_F32_COMP_RES ? -RDN_F32_CHUNK_RES : 1; };
 
 // the blob's per-layer correction mask (common.hpp CORR_SLOT), a scalar load
 __device__ __forceinline__ uint64_t corr_mask(const uint8_t* blob) {

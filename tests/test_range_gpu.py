@@ -9,13 +9,17 @@ by 10, 100 and 1000 through every arithmetic mode.  The reference takes any floa
   planes' range (|v| > 1792: the trained networks reach 9-28 at scale 1, ~300 at 10, ~3,000 at 100),
   and the saturated tiles are NaN.
 
-Judging fp32 at these scales: the networks become ill-conditioned (sigmoid heads, CBAM max pools, deep
+Judging fp32 at these scales: the networks become ill-conditioned (sigmoid heads, CBAM gating, deep
 residual sums), and the reference's own fp32 forward drifts from the exact (float64) one -- APIDN at 10x
-by 4e-3, ADSDN at 1000x by 1.6e-2 relative (measured).  So each result is held to the exact
-forward with the bar  max(1e-5 x max|y64|, 8 x |ref32 - y64|max): the north-star 1e-5, or a few times the
-reference's own rounding where that is larger (the engine's fp32 runs one plain fp32 chain per output on
-the residual networks, the reference oneDNN's blocking: at APIDN x1000 they sit 1.0e-3 and 2.0e-4 from
-float64).
+by 4e-3, ADSDN at 1000x by 39-50 of outputs ~2,500 (profiles/r05/ablate/fp32_rescomp.log).  At 1000x the
+CBAM networks are chaotic: the fp32 result's distance from float64 is a draw whose size depends on the
+summation order -- the same reference forward gives 39 on one host CPU and 50 on another, and fp32
+forwards whose weights differ by one rounding (1 ulp) give 10-52.  So the fp32 noise floor is taken as
+the largest distance from float64 of four fp32 oracle forwards: the reference weights and three 1-ulp
+perturbations of them; each result is held to the exact forward with the bar
+max(1e-5 x max|y64|, 2 x floor).  On the well-conditioned cases the floor is the reference's own
+distance within a factor ~2.  Every forward here comes from the oracle (oracle/models.py, the functional
+restatement pinned against the reference's fixtures), the float64 one on float64 weights and inputs.
 """
 import warnings
 
@@ -32,25 +36,35 @@ SCALES = [10.0, 100.0, 1000.0]
 _REFS = {}
 
 
+def _perturbed(sd, seed):
+    """the weights with every element moved by -1, 0 or +1 ulp of fp32 (seeded)"""
+    g = torch.Generator().manual_seed(seed)
+    return {k: (v * (1 + torch.randint(-1, 2, v.shape, generator=g).float() * 2.0 ** -24)).float()
+            if v.is_floating_point() and v.numel() > 1 else v for k, v in sd.items()}
+
+
 def _refs(arch, x):
-    """(fp32 reference, float64 exact) forwards of the trained network on x (CPU, the module's eager
-    path = the reference forward on the reference submodule tree; cached)."""
-    import raman_mi355x as R
+    """(fp32 noise floor, float64 exact forward) of the trained network on x (CPU oracle; cached): the
+    floor is the largest distance from float64 of the fp32 forward and of three 1-ulp perturbations."""
+    from oracle import models as om
     key = (arch, x.shape, float(np.abs(x).max()), float(x.ravel()[0]))
     if key not in _REFS:
         sd = golden_state_dict(arch, "trained")
-        m32, m64 = R.MODELS[arch](), R.MODELS[arch]()
-        m32.load_state_dict(sd, strict=True)
-        m64.load_state_dict(sd, strict=True)
-        m64 = m64.double()
+        sd64 = {k: v.double() if v.is_floating_point() else v for k, v in sd.items()}
         xt = torch.from_numpy(x).unsqueeze(1)
         with torch.no_grad():
-            _REFS[key] = (m32.eval()(xt).squeeze(1).numpy(), m64.eval()(xt.double()).squeeze(1).numpy())
+            y64 = om.FORWARD[arch](sd64, xt.double()).squeeze(1).numpy()
+            floor = max(float(np.abs(om.forward(arch, w, xt).squeeze(1).numpy() - y64).max())
+                        for w in [sd] + [_perturbed(sd, s) for s in range(3)])
+        _REFS[key] = (floor, y64)
     return _REFS[key]
 
 
-def _bar(ref32, y64):
-    return max(1e-5 * float(np.abs(y64).max()), 8.0 * float(np.abs(ref32 - y64).max()))
+FACTOR = 2.0      # x the fp32 noise floor (VERDICT r04 item 7: was 8 x the reference's own distance)
+
+
+def _bar(floor, y64):
+    return max(1e-5 * float(np.abs(y64).max()), FACTOR * floor)
 
 
 def _x(inputs):
@@ -69,7 +83,7 @@ def test_module_matches_exact_forward_on_scaled_inputs(arch, dtype, scale, input
     m = m.cuda().eval().set_engine_dtype(dtype)
     for x in _x(inputs):
         xs = (x * scale).astype(np.float32)
-        ref32, y64 = _refs(arch, xs)
+        floor, y64 = _refs(arch, xs)
         m._range_warned = False                # the module warns once; re-arm it per input
         with torch.no_grad(), warnings.catch_warnings(record=True) as w:
             warnings.simplefilter("always", RuntimeWarning)
@@ -78,7 +92,7 @@ def test_module_matches_exact_forward_on_scaled_inputs(arch, dtype, scale, input
         if dtype != "fp32":                   # beyond the 16-bit domain: the module ran fp32
             assert any("ran in fp32" in str(r.message) for r in w), (arch, dtype, scale)
         err = float(np.abs(y - y64).max())
-        assert err <= _bar(ref32, y64), (arch, dtype, scale, err, _bar(ref32, y64))
+        assert err <= _bar(floor, y64), (arch, dtype, scale, err, _bar(floor, y64))
 
 
 @pytest.mark.parametrize("dtype", ["f16f8", "f16"])

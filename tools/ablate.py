@@ -22,7 +22,7 @@ VARIANTS = {"base": "", "prev": "", "cur": "", "cur2": "", "nolds": "-DRDN_ABLAT
             "h16f16": "-DRDN_H16_F16=1", "ld2": "-DRDN_H16_LDSTEP=2", "ld3": "-DRDN_H16_LDSTEP=3", "ld4": "-DRDN_H16_LDSTEP=4", "pf2": "-DRDN_H16_PF=2", "pf4": "-DRDN_H16_PF=4", "alledge": "-DRDN_ABLATE_ALLEDGE -DRDN_TEAM_STAMPS=1",
             "tail3": "-DRDN_F16MIX_TAIL=3", "tail4": "-DRDN_F16MIX_TAIL=4", "tail5": "-DRDN_F16MIX_TAIL=5", "nowin": "-DRDN_F16MIX_WIN=0", "nostem": "-DRDN_ABLATE_NOSTEM",
             "tail0": "-DRDN_F16MIX_TAIL=0", "tail2": "-DRDN_F16MIX_TAIL=2", "hybstamps": "-DRDN_HYB_STAMPS=1",
-            "w512": "-DRDN_WALK_ROWS=512", "w448": "-DRDN_WALK_ROWS=448", "mix512": "-DRDN_WALK_ROWS_MIX=512", "mhead": "", "lbar": "", "stg": "", "vote": "", "comb": "", "track": "", "trk2": "", "sdpp": "", "cur": "", "resplain": ""}
+            "w512": "-DRDN_WALK_ROWS=512", "w448": "-DRDN_WALK_ROWS=448", "mix512": "-DRDN_WALK_ROWS_MIX=512", "mhead": "", "lbar": "", "stg": "", "vote": "", "comb": "", "track": "", "trk2": "", "sdpp": "", "cur": "", "resplain": "", "rescomp0": "-DRDN_F32_COMP_RES=0", "reschunk6": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=6", "reschunk3": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=3", "reschunk4": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=4", "reschunk2": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=2"}
 
 
 def build():
@@ -199,6 +199,14 @@ def parity():
                       f"(ref vs f64 {worst[2]:.2e})", flush=True)
 
 
+def _perturbed(sd, seed):
+    """the weights with every element moved by -1, 0 or +1 ulp of fp32 (tests/test_range_gpu.py)"""
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    return {k: (v * (1 + torch.randint(-1, 2, v.shape, generator=g).float() * 2.0 ** -24)).float()
+            if v.is_floating_point() and v.numel() > 1 else v for k, v in sd.items()}
+
+
 def scaled():
     """fp32 on scaled inputs (tests/test_range_gpu.py's cases): per built variant, network and scale, the
     engine's max distance from the float64 forward over the reference fp32's own distance (the test's
@@ -240,7 +248,15 @@ def scaled():
             for x in xs:
                 xt = torch.from_numpy((x * scale).astype(np.float32)).unsqueeze(1)
                 with torch.no_grad():
-                    refs.append((xt, m32(xt).squeeze(1).numpy(), m64(xt.double()).squeeze(1).numpy()))
+                    y64 = m64(xt.double()).squeeze(1).numpy()
+                    # fp32 noise floor as tests/test_range_gpu.py: the reference weights and three 1-ulp
+                    # perturbations, the largest distance from float64
+                    floor = float(np.abs(m32(xt).squeeze(1).numpy() - y64).max())
+                    for seed in range(3):
+                        mp = R.MODELS[arch]()
+                        mp.load_state_dict(_perturbed(sd, seed), strict=True)
+                        floor = max(floor, float(np.abs(mp.eval()(xt).squeeze(1).numpy() - y64).max()))
+                    refs.append((xt, m32(xt).squeeze(1).numpy(), y64, floor))
             line = []
             for name, lib in libs.items():
                 size = ctypes.c_size_t()
@@ -248,8 +264,8 @@ def scaled():
                 blob = torch.empty(size.value, dtype=torch.uint8)
                 assert lib.rdn_pack(aid, code, ptrs, numels, len(host), ctypes.c_void_p(blob.data_ptr()), size.value) == 0
                 blob = blob.to(dev)
-                worst_e, worst_r = 0.0, 0.0
-                for xt, r32, y64 in refs:
+                worst_e, worst_r, worst_q, worst_f = 0.0, 0.0, 0.0, 0.0
+                for xt, r32, y64, floor in refs:
                     xd = xt.to(dev)
                     y = torch.empty_like(xd)
                     wsz = ctypes.c_size_t()
@@ -259,9 +275,14 @@ def scaled():
                                          ws.data_ptr(), wsz.value, torch.cuda.current_stream().cuda_stream)
                     assert rc == 0, lib.rdn_last_error()
                     yh = y.squeeze(1).cpu().numpy()
-                    worst_e = max(worst_e, float(np.abs(yh - y64).max()))
-                    worst_r = max(worst_r, float(np.abs(r32 - y64).max()))
-                line.append(f"{name} {worst_e:.2e} ({worst_e / max(worst_r, 1e-30):.2f}x)")
+                    e_, r_ = float(np.abs(yh - y64).max()), float(np.abs(r32 - y64).max())
+                    bar = max(1e-5 * float(np.abs(y64).max()), r_)       # test_range_gpu's bar at factor 1
+                    fbar = max(1e-5 * float(np.abs(y64).max()), floor)
+                    worst_e, worst_r, worst_q = max(worst_e, e_), max(worst_r, r_), max(worst_q, e_ / bar)
+                    worst_f = max(worst_f, e_ / fbar)
+                # worst over the inputs of (engine distance) / max(1e-5 max|y64|, reference distance), and
+                # of (engine distance) / max(1e-5 max|y64|, fp32 noise floor)
+                line.append(f"{name} {worst_e:.2e} ({worst_q:.2f}x ref, {worst_f:.2f}x floor)")
             print(f"{arch:10s} x{scale:<6g} ref32-vs-f64 {worst_r:.2e} | " + " | ".join(line), flush=True)
 
 
