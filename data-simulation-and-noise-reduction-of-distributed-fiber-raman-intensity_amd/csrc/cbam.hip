@@ -1295,11 +1295,13 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
           __builtin_elementwise_max(__builtin_shufflevector(vm, vm, 0, 1), __builtin_shufflevector(vm, vm, 2, 3)),
           __builtin_elementwise_max(__builtin_shufflevector(vm, vm, 4, 5), __builtin_shufflevector(vm, vm, 6, 7)));
       const float mx = quarter_max(fmaxf((float)x2[0], (float)x2[1]));
+      // (rows at positions outside [0, L) hold u = 0 -- conv2's zero_outside, and no neighbour refreshes
+      // an edge tile's outer halo -- so their mean and max come out 0, the map's zero padding, with no
+      // per-row check)
       if (ln.q == 0) {
         const int r = SROWS * w + ln.c16 + 16 * k;
-        const bool in = !EDGE || h16c::in_range(tl.base + r, tl.L);
-        m1[r] = in ? sm * (1.0f / 64.0f) : 0.f;
-        m2[r] = in ? mx : 0.f;
+        m1[r] = sm * (1.0f / 64.0f);
+        m2[r] = mx;
       }
     }
     if (tid < 6) {                             // rows beyond the tile feed only halo rows: 0
@@ -1336,7 +1338,9 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   __syncthreads();
   st(13);
   V uv[NT];
-  // h = [identity +] u*ca*sa [relu], in place, packed f16; rows outside [0, L) zero
+  // h = [identity +] u*ca*sa [relu], in place, packed f16.  Rows at positions outside [0, L) stay zero
+  // without a check: u is 0 there (conv2's zero_outside; the stem's for the first CBAM), ca and sa are
+  // finite, and the identity -- the block input, an earlier h -- is 0 there too
   float sv[NT];
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
@@ -1345,14 +1349,12 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   }
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
-    const int r = ln.row(n);
     V* pu = (V*)(b0 + n * 16 * h16c::ROWB);
     V hv = (uv[n] * cah) * (V)((_Float16)sv[n]);
     if (res != RES_NONE) {
       hv += idv[n];
       if (res == RES_ADD_RELU) hv = __builtin_elementwise_max(hv, (V)((_Float16)0));
     }
-    if (EDGE && !h16c::in_range(tl.base + r, tl.L)) hv = (V)((_Float16)0);
     *pu = hv;
   }
   __syncthreads();

@@ -608,7 +608,9 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     prev = acc;
   }
   epilogue(NT - 1, prev);
+#if !defined(RDN_ABLATE_NOZERO)           // diagnostic builds only (tools/ablate.py): wrong results
   if constexpr (EDGE && EPI != STAGE) zero_outside(tl, dst, pos0 - tl.base, h, lane);
+#endif
   // walk: the next layer's (RES_RELU) N-tile-0 identity, rows r0 - 2 of this layer's input (stable
   // until the barrier below)
   if (WALK && walk_id) *walk_id = *(const V*)(tl.lds + src + (h ? tl.koff[2][1] : tl.koff[2][0]));

@@ -68,13 +68,22 @@ def main():
     # team the others wait for (TT from L: 640-row tiles with 6-row halos)
     tt = -(-L // 628)
     wg = torch.arange(256)[used]
+    # team16_forward's XCD-aware placement: workgroups 8r + x, r < R0, are tile r % TT of a team on XCD x
+    teams = int(used.sum()) // tt
+    r0 = ((teams * tt // 8) // tt) * tt
     byt = {}
     for i, g in zip(wg.tolist(), st[used]):
-        byt.setdefault(i % tt, []).append(g)
+        t = (i >> 3) % tt if i < 8 * r0 else (i - 8 * r0) % tt
+        byt.setdefault(t, []).append(g)
     print("per tile: conv cycles / poll cycles (mean over teams)")
     for t in sorted(byt):
         g = torch.stack(byt[t])
         print(f"  tile {t:2d}: conv {g[:, 1].mean():.4e}  poll {g[:, 10].mean() + g[:, 4].mean():.4e}")
+    print("per phase: edge tiles 0 / TT-1 against interior tile 1 (mean over teams)")
+    for k, p in enumerate(PHASES):
+        m = [torch.stack(byt[t])[:, k].mean().item() for t in (0, 1, tt - 1)]
+        if max(m) > 0:
+            print(f"  {p:18s} tile0 {m[0]:.4e}  tile1 {m[1]:.4e}  tile{tt - 1} {m[2]:.4e}  (edge - interior: {m[0] - m[1]:+.3e} / {m[2] - m[1]:+.3e})")
     st = st[used]
     tot = st.sum(1)
     print(f"[{variant}] {arch} {dtype} L={L} B={B}: {ms:.2f} ms, {B / ms * 1e3:,.0f} spectra/s, {int(used.sum())} workgroups")
