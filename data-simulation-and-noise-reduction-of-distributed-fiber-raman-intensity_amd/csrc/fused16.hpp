@@ -184,16 +184,20 @@ __device__ __forceinline__ LaneOff lane_off() {
   const int lane = tid() & 63;
   return {lane * 16, (lane >> 4) * 16};
 }
-// operand i of half h of big layer `layer`: A-fragment i (< NFRAG) or bias vector i - NFRAG
+// operand i of half h of big layer `layer`, in the order of first use: the two bias vectors (the
+// accumulators' start at k-step 0), then the A-fragments by k-step, both M-tiles of a step together.
+// The loads are counted in order (vmcnt), so the operands issued last -- those of k-step 5 -- are the
+// ones the next layer needs last (bias last: the next layer's first MFMA waited on the load issued
+// two steps before the barrier).
 __device__ __forceinline__ void load_op(const Tile& tl, int layer, int h, int i, const LaneOff& lo, Frags& F) {
   const int base = layer * LAYER_BYTES;
-  if (i < NFRAG) {
-    const int so = base + ((2 * h + i / 6) * 6 + i % 6) * 1024;
-    F.a[i] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, lo.a, so, 0));
+  if (i < NBIAS) {
+    const int so = base + BIAS_OFF + 64 * (2 * h + i);
+    F.bias[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, lo.b, so, 0));
   } else {
-    const int j = i - NFRAG;
-    const int so = base + BIAS_OFF + 64 * (2 * h + j);
-    F.bias[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, lo.b, so, 0));
+    const int f = i - NBIAS, m = f & 1, s = f >> 1;
+    const int so = base + ((2 * h + m) * 6 + s) * 1024;
+    F.a[m * 6 + s] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(tl.wrsrc, lo.a, so, 0));
   }
 }
 constexpr int NLOAD = NFRAG + NBIAS;
