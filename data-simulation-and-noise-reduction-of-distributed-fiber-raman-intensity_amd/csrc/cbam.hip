@@ -1360,17 +1360,31 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   __syncthreads();
 }
 
+// The spectra of team `team`: a contiguous range.  Teams 0 .. nloc-1 sit on one XCD each; the rest
+// (L = 16,384: 27-tile teams, 9 per chip, the ninth spread over the XCDs' spare CUs) hand off across
+// XCDs and run ~3 % slower per spectrum (tools/team_stamps.py: 4.61e7 vs 4.47e7 cycles), so with
+// XCD-local hand-offs they take 31/32 of a local team's share and the launch's teams finish together.
+__device__ __forceinline__ void team_range(const TeamArgs& ta, int team, int nloc, int64_t& lo, int64_t& hi) {
+  const int64_t ws = ta.xcd && nloc < ta.teams ? 31 : 32;
+  auto cum = [&](int t) -> int64_t { return t <= nloc ? 32LL * t : 32LL * nloc + ws * (t - nloc); };
+  const int64_t W = cum(ta.teams);
+  lo = (ta.n * cum(team) + W - 1) / W;         // rounded up: with fewer spectra than teams, team 0
+  hi = (ta.n * cum(team + 1) + W - 1) / W;     // takes spectrum 0
+}
+
 template <bool ADS, bool EDGE>
 __device__ __forceinline__ void team16_spectra(char* lds, const uint8_t* blob, const uint8_t* big16, const float* x,
                                                float* y, int L, const TeamArgs& ta, int team, int tile,
-                                               bool local) {
+                                               bool local, int nloc) {
   unsigned* ctr = ta.counters + (size_t)team * TEAM_CTR_STRIDE;
   int xmode = ta.xcd ? XM_PROBE : XM_SC1;
   char* tslots = ta.slots + (size_t)team * 2 * ta.TT * SLOT16_BYTES;
   unsigned nbar = 0;
   Stamps st;
   st.init();
-  for (int64_t n = team; n < ta.n; n += ta.teams) {
+  int64_t n_lo, n_hi;
+  team_range(ta, team, nloc, n_lo, n_hi);
+  for (int64_t n = n_lo; n < n_hi; ++n) {
     h16c::Tile tl = h16c::init_tile(lds, blob, big16, x + (size_t)n * L, L, tile * ta.T - ta.halo);
     h16c::Frags F0, F1;
     V id[NT];
@@ -1463,11 +1477,11 @@ __global__ __launch_bounds__(h16c::THREADS) void team16_forward(const uint8_t* _
   const int base = tile * ta.T - ta.halo;
   // a tile holds positions outside [0, L) for every spectrum or for none (one L per launch)
 #if defined(RDN_ABLATE_ALLEDGE)          // diagnostic: every tile on the edge-tile code
-  if (false) t16::team16_spectra<ADS, false>(lds, blob, big16, x, y, L, ta, team, tile, local);
+  if (false) t16::team16_spectra<ADS, false>(lds, blob, big16, x, y, L, ta, team, tile, local, 8 * tpx);
 #else
-  if (base >= 0 && base + t16::WB16 <= L) t16::team16_spectra<ADS, false>(lds, blob, big16, x, y, L, ta, team, tile, local);
+  if (base >= 0 && base + t16::WB16 <= L) t16::team16_spectra<ADS, false>(lds, blob, big16, x, y, L, ta, team, tile, local, 8 * tpx);
 #endif
-  else t16::team16_spectra<ADS, true>(lds, blob, big16, x, y, L, ta, team, tile, local);
+  else t16::team16_spectra<ADS, true>(lds, blob, big16, x, y, L, ta, team, tile, local, 8 * tpx);
 }
 
 }  // namespace cb

@@ -79,6 +79,16 @@ def main():
     for t in sorted(byt):
         g = torch.stack(byt[t])
         print(f"  tile {t:2d}: conv {g[:, 1].mean():.4e}  poll {g[:, 10].mean() + g[:, 4].mean():.4e}")
+    # per team: total cycles (mean / max over its tiles); teams >= 8 * (r0 // tt) are the ones not
+    # confined to one XCD
+    byteam = {}
+    for i, g in zip(wg.tolist(), st[used]):
+        team = ((i >> 3) // tt) * 8 + (i & 7) if i < 8 * r0 else 8 * (r0 // tt) + (i - 8 * r0) // tt
+        byteam.setdefault(team, []).append(g.sum().item())
+    print("per team: total cycles mean / max over its tiles (spectra per team: %d)" % -(-1024 // teams))
+    for tm in sorted(byteam):
+        v = byteam[tm]
+        print(f"  team {tm:2d}{' (spread)' if tm >= 8 * (r0 // tt) else ''}: {sum(v) / len(v):.4e} / {max(v):.4e}")
     print("per phase: edge tiles 0 / TT-1 against interior tile 1 (mean over teams)")
     for k, p in enumerate(PHASES):
         m = [torch.stack(byt[t])[:, k].mean().item() for t in (0, 1, tt - 1)]
