@@ -19,7 +19,7 @@ if [[ " $STAGES " == *" parity "* ]]; then
   timeout -k 10 300 python -u tools/parity_report.py --out $OUT/parity.md > $OUT/parity.log 2>&1
   rc=$?; tail -2 $OUT/parity.md; if [ $rc -ne 0 ]; then exit $rc; fi
 fi
-INNER="$(echo " $STAGES " | grep -o ' bench \| kt \| pmc ' | tr -d '\n')"
+INNER="$(echo "$STAGES" | tr ' ' '\n' | grep -x 'bench\|kt\|pmc' | tr '\n' ' ')"
 if [ -n "$INNER" ]; then
   STAGES="$INNER" bash scripts/gpu_final.sh
   rc=$?; if [ $rc -ne 0 ]; then exit $rc; fi
