@@ -178,3 +178,30 @@ def test_no_false_range_error_after_saturated_launch(dtype, short, inputs, monke
             y = engine.forward("RRCDNet", code, packed, x, check=False, workspace=ws)
             ws.check()                                           # no RangeError
             assert torch.isfinite(y).all(), (dtype, short, L, B)
+
+
+@pytest.mark.parametrize("arch,dtype,scale", [("RRCDNet", "f16", 100.0), ("DSDN", "f16f8", 1000.0),
+                                              ("ADSDN", "f16f8", 1000.0)])
+def test_range_signal_survives_flush_denormal(arch, dtype, scale, inputs):
+    """the module reads the status word as an integer (the kernels set bit 0 = 1u, a float
+    denormal), so the host's denormals-are-zero mode (torch.set_flush_denormal(True)) cannot hide the
+    range signal: a saturating batch is still re-run in fp32 and returned without NaN."""
+    import raman_mi355x as R
+    sd = golden_state_dict(arch, "trained")
+    m = R.MODELS[arch]()
+    m.load_state_dict(sd, strict=True)
+    m = m.cuda().eval().set_engine_dtype(dtype)
+    ref = R.MODELS[arch]()
+    ref.load_state_dict(sd, strict=True)
+    ref = ref.cuda().eval()
+    x = torch.from_numpy((inputs["main_noisy"][:2] * scale).astype(np.float32)).unsqueeze(1).cuda()
+    if not torch.set_flush_denormal(True):
+        pytest.skip("this host CPU has no denormals-are-zero mode")
+    try:
+        with torch.no_grad(), pytest.warns(RuntimeWarning, match="ran in fp32"):
+            y = m(x)
+    finally:
+        torch.set_flush_denormal(False)
+    with torch.no_grad():
+        assert torch.equal(y, ref(x))
+    assert torch.isfinite(y).all()
