@@ -522,12 +522,17 @@ __device__ __forceinline__ void publish_stats(const Tile& tl, const TeamArgs& ta
   }
   float* rs = (float*)(lds + RED_OFF);
   unsigned* rm = (unsigned*)(lds + RED_OFF + 8 * 64 * 8);
+  unsigned* rsat = (unsigned*)(lds + RED_OFF + 8 * 64 * 4);       // per-wave saturation votes (MODE_H8)
   if (rgrp == 0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       rs[w * 64 + 4 * sub + i] = sm[i];
       rm[w * 64 + 4 * sub + i] = f2ord(mx[i]);
     }
+  }
+  if constexpr (MODE == MODE_H8) {
+    const bool wave_sat = __builtin_amdgcn_ballot_w64(tl.amax > H8_SAT) != 0;
+    if (lane == 0) rsat[w] = wave_sat ? 1u : 0u;
   }
   // the edge stores drain under the statistics pass; every storing wave waits for them before the
   // barrier that precedes the arrival
@@ -543,6 +548,14 @@ __device__ __forceinline__ void publish_stats(const Tile& tl, const TeamArgs& ta
     for (int k = 0; k < WAVES; ++k) {
       s += (double)rs[k * 64 + c];
       m = max(m, rm[k * 64 + c]);
+    }
+    // MODE_H8: a tile whose activations saturated so far publishes +inf maxima -- stored activations
+    // are clamped to +-1792, so an infinite pooled maximum taints the whole team's spectrum (apply_cbam)
+    if constexpr (MODE == MODE_H8) {
+      bool sat = false;
+#pragma unroll
+      for (int k = 0; k < WAVES; ++k) sat = sat || rsat[k] != 0;
+      if (sat) m = f2ord(INFINITY);
     }
     __hip_atomic_store((double*)slot + c, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store((unsigned*)(slot + 512) + c, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -584,8 +597,9 @@ constexpr int ID_ITERS = WB / (WAVES * 4);          // rows per thread in the po
 // spectra/s); plain bf16 keeps its identity in LDS
 template <int MODE> constexpr int ID_PRE = MODE == MODE_X3 ? 8 : 16;
 
+// Returns whether a tile of the team had saturated (MODE_H8: an infinite pooled maximum, publish_stats).
 template <int MODE>
-__device__ __forceinline__ void apply_cbam(Tile& tl, const TeamArgs& ta, const char* slots0, int cbam_slot, bool bias, int res,
+__device__ __forceinline__ bool apply_cbam(Tile& tl, const TeamArgs& ta, const char* slots0, int cbam_slot, bool bias, int res,
                            bool save_next, __amdgpu_buffer_rsrc_t hs, Stamps& st) {
   char* lds = tl.lds;
   float* s1 = (float*)(lds + S1_OFF) + 3;       // index -3 .. 514
@@ -670,6 +684,8 @@ __device__ __forceinline__ void apply_cbam(Tile& tl, const TeamArgs& ta, const c
   if (has_edge) Op<MODE>::store4(lds, (edge_e == 0 ? edge_k : WB - EDGE_ROWS + edge_k) + GUARD, 4 * (tid & 15), edge_u);
   __syncthreads();
   st(10);
+  // MODE_H8: a tile of the team that saturated (its +inf maxima, publish_stats) taints the spectrum
+  const bool taint = MODE == MODE_H8 && red[64] == (double)INFINITY;
   // -- channel attention: hidden unit (w & 3) of the shared MLP for the avg (w < 4) or max pooled
   //    vector, one wave each (64 lanes = 64 channels, butterfly sum)
   {
@@ -755,6 +771,7 @@ __device__ __forceinline__ void apply_cbam(Tile& tl, const TeamArgs& ta, const c
     if (save_next) id_store<MODE>(lds, hs, r, sub, h);
   }
   __syncthreads();
+  return taint;
 }
 
 template <int MODE, bool ADS>
@@ -789,6 +806,7 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
     tl.status = nullptr;
     LayerA<MODE> a;
     load_layer_a<MODE>(tl, 0, a);
+    bool tainted = false;                 // MODE_H8: a tile of this spectrum saturated (apply_cbam)
     // stats of u -> team -> apply.  The identity rows are fetched while the team assembles; the
     // next layer's operands are loaded only now (held across this VALU-heavy code they spill).
     auto cbam = [&](int slot, int res, bool save_next) {
@@ -798,7 +816,8 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
       stamp(3);
       team_wait(ta, ctr, (nbar + 1) * (unsigned)ta.TT);
       stamp(4);
-      apply_cbam<MODE>(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT_BYTES, slot, ADS, res, save_next, hs, stamp);
+      tainted = apply_cbam<MODE>(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT_BYTES, slot, ADS, res, save_next, hs,
+                                 stamp) || tainted;
       stamp(5);
       ++nbar;
       if (RELOAD_A && tl.layer < NL) load_layer_a<MODE>(tl, tl.layer, a);
@@ -849,7 +868,9 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
     // MODE_H8 range guard: a tile whose activations saturated raises the sticky range word (err[2],
     // the authoritative signal: its CBAM statistics reached the whole team) and writes NaN
     if constexpr (MODE == MODE_H8) {
-      if (range_vote(tl, RED_OFF, ta.err + 2)) nan_rows(v);
+      // (and every other tile of a spectrum one of whose tiles saturated: its clamped statistics
+      // reached them through the hand-offs -- the whole spectrum is NaN, not just that tile)
+      if (range_vote(tl, RED_OFF, ta.err + 2) || tainted) nan_rows(v);
     }
     store_out<MODE>(tl, y, (int)n, v, ta.halo, ta.T);
     __syncthreads();                 // the next spectrum's stem overwrites the rows the head read

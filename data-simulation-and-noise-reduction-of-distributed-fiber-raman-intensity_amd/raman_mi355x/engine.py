@@ -259,11 +259,12 @@ def forward(arch, dtype, packed, x, out=None, check=True, workspace=None, _ws_ch
     ``check=False`` and calls ``workspace.check()`` once at the end (the status words are sticky);
     (``_ws_checked``: the caller has just verified ``workspace.fits`` for this input.)
     ``check=False`` without a workspace keeps the launch asynchronous and unchecked (benchmarks: the
-    affected outputs are NaN).  On the CBAM networks (ADSDN / APIDN) a saturated tile is NaN, but its
-    clamped CBAM statistics have already reached the other tiles of its spectrum through the team
-    hand-off: those outputs are finite and wrong.  There the status word (RangeError from ``check`` or
-    ``Workspace.check()``), not the absence of NaN, is the authoritative signal -- never run a CBAM
-    network with ``check=False`` and no later ``Workspace.check()`` on data that might saturate."""
+    affected outputs are NaN).  On the CBAM networks (ADSDN / APIDN) a saturated tile's clamped CBAM
+    statistics reach the other tiles of its spectrum through the team hand-off, so the whole spectrum
+    is NaN, not just the tile: the team kernel's saturated tile publishes +inf maxima that taint its
+    team (cbam.hip publish_stats / apply_cbam), and a segment-path launch (spectra longer than the
+    co-resident teams hold) NaNs every spectrum of the chunk.  The status word (RangeError from
+    ``check`` or ``Workspace.check()``) remains the authoritative signal."""
     _check_cuda_f32(x, "input")
     if x.dim() == 3 and x.shape[1] != 1:
         raise ValueError(f"expected (N, 1, L) input, got {tuple(x.shape)}")

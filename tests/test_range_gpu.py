@@ -205,3 +205,40 @@ def test_range_signal_survives_flush_denormal(arch, dtype, scale, inputs):
     with torch.no_grad():
         assert torch.equal(y, ref(x))
     assert torch.isfinite(y).all()
+
+
+@pytest.mark.parametrize("arch", ["ADSDN", "APIDN"])
+def test_cbam_saturation_taints_whole_spectrum(arch, inputs):
+    """in the CBAM team kernel (f16f8) a saturated tile's clamped statistics reach every tile
+    of its spectrum through the hand-offs, so a saturated spectrum is NaN at every position -- never
+    finite-but-wrong tiles beside NaN ones -- while spectra without a saturated tile stay finite and
+    equal to the same launch without the saturated spectrum."""
+    import raman_mi355x as R
+    from raman_mi355x import _lib, engine
+    sd = golden_state_dict(arch, "trained")
+    m = R.MODELS[arch]()
+    m.load_state_dict(sd, strict=True)
+    m = m.cuda().eval().set_engine_dtype("f16f8")
+    code = m.engine_code
+    base = inputs["main_noisy"][:2]
+    packed = m.packed_weights(torch.device("cuda"))
+    for scale in (10.0, 100.0, 1000.0):
+        # spectrum 0 scaled, spectrum 1 normal: one launch, separate teams
+        xs = np.stack([base[0] * scale, base[1]]).astype(np.float32)
+        x = torch.from_numpy(xs).unsqueeze(1).cuda()
+        ws = engine.Workspace(arch, code, 2, x.shape[-1], x.device)
+        y = engine.forward(arch, code, packed, x, check=False, workspace=ws).squeeze(1).cpu().numpy()
+        try:
+            ws.check()
+            saturated = False
+        except _lib.RangeError:
+            saturated = True
+        fin = np.isfinite(y)
+        print(f"{arch} x{scale:g}: saturated {saturated}, finite fraction {fin[0].mean():.3f} / {fin[1].mean():.3f}")
+        assert fin[0].all() or not fin[0].any(), (arch, scale, fin[0].mean())
+        assert fin[1].all(), (arch, scale)
+        assert saturated == (not fin[0].all()), (arch, scale)
+    assert saturated, arch                                        # x1000 saturates (test above)
+    x1 = torch.from_numpy(base[1:2].astype(np.float32)).unsqueeze(1).cuda()
+    y1 = engine.forward(arch, code, packed, x1, check=True).squeeze(1).cpu().numpy()
+    assert np.array_equal(y1[0], y[1]), arch
