@@ -15,7 +15,7 @@
 //
 // Each Conv1d(64,64,3,d) is an implicit GEMM  Y[64 cout][640 pos] = W[64][192] . X~[192][640]
 // whose B operand is read straight from the activation buffer at row offsets (t-1)*d (no
-// im2col).  Wave w owns row block w % 4 (RW = 160 rows, NT = 10 N-tiles) and output channels
+// im2col).  Wave w owns row block w % 4 (RW = 160 rows, NT = 10 N-tiles; walk: rblock) and output channels
 // 32h .. 32h+31 (h = w / 4: two M-tiles), so the two waves of a SIMD (w, w + 4) split the output
 // channels of the same rows.  The split halves the weights a wave holds (12 A-fragments, 12 KB per
 // layer, loaded from L2/L1 by every wave: 96 KB per CU per layer instead of 192 KB -- the vector
@@ -154,7 +154,7 @@ struct Tile {
   int layer;             // big layer whose fragments are in VGPRs
   // per-lane LDS offsets, computed once per tile (no address arithmetic at each layer's start):
   // koff[d + 2][u] = soff(r0 + d, 4u + q) for tap shift d in -2..2 (no wrap), r0 = this lane's
-  // first row ((w % RB) * RW + lane % 16); walk: koff[d + 4][u] for d in -4..0, r0 = CG + ...
+  // first row (rblock(w) * RW + lane % 16); walk: koff[d + 4][u] for d in -4..0, r0 = CG + ...
   int koff[5][KS / 3];
   int r0;
   // walk only (layer_carry): the carry slot of the layer being computed (its last 2 dnext rows, for
@@ -171,6 +171,13 @@ struct Frags {            // one layer's operands in VGPRs: this wave's A-fragme
 };
 // this wave's output-channel half (channels 32h .. 32h + 31), wave-uniform
 __device__ __forceinline__ int mhalf() { return __builtin_amdgcn_readfirstlane(tid() >> 6) / RB; }
+// the row block of wave w (channel half w / RB).  Tiles: w % RB.  Walk: the second half's row blocks
+// are rotated by two, so the two waves a SIMD holds (w and w + 4: a workgroup's waves go to its
+// SIMDs cyclically, MI355X_MICROARCH.md §LDS) own row blocks two apart -- on a spectrum's short last
+// tile, whose upper row blocks lie beyond L and skip their MFMAs, every SIMD keeps one busy wave
+// instead of two SIMDs carrying both waves of the live row blocks
+static_assert(!WALK || (RB == 4 && MH == 2), "the walk's row-block rotation is written for 4 x 2 waves");
+__device__ __forceinline__ int rblock(int w) { return WALK ? (w + 2 * (w / RB)) % RB : w % RB; }
 
 // Operand loads as raw buffer loads: lane offset in a VGPR, layer/fragment offset in an SGPR, so
 // the loads of a layer cost no address VALU.
@@ -452,7 +459,7 @@ struct Carry {
 __device__ __forceinline__ Carry carry_load(const Tile& tl, uint32_t src, bool has_dst) {
   Carry c;
   const int w = __builtin_amdgcn_readfirstlane(tid() >> 6), lane = tid() & 63;
-  if (w % RB == RB - 1) {
+  if (rblock(w) == RB - 1) {
     const int k = lane >> 2, g = 4 * (w / RB) + (lane & 3);
     if (has_dst && k < 2 * tl.dnext)
       c.a = tl.first ? (V)((E)0) : *(const V*)(tl.lds + tl.cs_cur + k * ROWB + 16 * g);
@@ -463,7 +470,7 @@ __device__ __forceinline__ Carry carry_load(const Tile& tl, uint32_t src, bool h
 // rowb: bytes per carry row of this layer's slot (the staged layer's outputs are 256-B plane rows)
 __device__ __forceinline__ void carry_store(Tile& tl, uint32_t dst, bool has_dst, const Carry& c, int rowb = ROWB) {
   const int w = __builtin_amdgcn_readfirstlane(tid() >> 6), lane = tid() & 63;
-  if (w % RB == RB - 1) {
+  if (rblock(w) == RB - 1) {
     const int k = lane >> 2, g = 4 * (w / RB) + (lane & 3);
     if (has_dst && k < 2 * tl.dnext) *(V*)(tl.lds + dst + soff(CG - 2 * tl.dnext + k, g)) = c.a;
     if (k < 2 * tl.dn_prev) *(V*)(tl.lds + tl.cs_prev + k * ROWB + 16 * g) = c.b;
@@ -493,7 +500,7 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     tl.base -= dil;                          // this layer's outputs: positions shifted by its dilation
     cc = carry_load(tl, src, CA);
   }
-  const int pos0 = tl.base + CG + (w % RB) * RW;
+  const int pos0 = tl.base + CG + rblock(w) * RW;
 
   // Idle waves of a short last tile: every row of this wave lies at position >= L + 2, beyond the
   // reach (d <= 2) of any row that matters, so it skips the layer's MFMAs and only zeroes its dst
@@ -644,7 +651,7 @@ __device__ __forceinline__ void head(Tile& tl, uint32_t src, const Frags& F, Fra
     tl.base -= 1;
     cc = carry_load(tl, src, false);
   }
-  const int pos0 = tl.base + CG + (w % RB) * RW + NR * HN * h;
+  const int pos0 = tl.base + CG + rblock(w) * RW + NR * HN * h;
   if (EDGE && pos0 >= tl.L + (WALK ? 0 : 2)) {
     if constexpr (WALK) carry_store(tl, 0, false, cc);
     if (has_next) load_frags(tl, next, G);
@@ -702,7 +709,7 @@ __device__ __forceinline__ Tile init_tile(char* lds, const uint8_t* blob, const 
   tl.layer = 0;
   const int t = tid();
   const int q = (t & 63) >> 4;
-  tl.r0 = CG + ((t >> 6) % RB) * RW + (t & 15);
+  tl.r0 = CG + rblock(t >> 6) * RW + (t & 15);
   constexpr int D0 = WALK ? -4 : -2;
 #pragma unroll
   for (int d = 0; d < 5; ++d)
@@ -727,7 +734,7 @@ __device__ __forceinline__ Tile make_tile(char* lds, const uint8_t* blob, const 
 // skipped N-tile of an odd NT
 __device__ __forceinline__ int head_row(int j) {
   const int w = tid() >> 6, n = HN * (w / RB) + j;
-  return n < NT ? CG + (w % RB) * RW + NR * n + (tid() & (HEAD_LANES - 1)) : WB;
+  return n < NT ? CG + rblock(w) * RW + NR * n + (tid() & (HEAD_LANES - 1)) : WB;
 }
 
 __device__ __forceinline__ void store_out(const Tile& tl, float* y, int n, const float (&v)[HN], int halo, int T) {

@@ -46,7 +46,7 @@ struct H8Stage {
   __device__ __forceinline__ void write(char* lds, const PP::Tile& t) const {
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     const int tid = PP::tid(), w = tid >> 6, lane = tid & 63;
-    const int g = 4 * (w / PP::RB) + (lane >> 4), r0 = PP::CG + (w % PP::RB) * PP::RW + (lane & 15);
+    const int g = 4 * (w / PP::RB) + (lane >> 4), r0 = PP::CG + PP::rblock(w) * PP::RW + (lane & 15);
 #pragma unroll
     for (int n = 0; n < PP::NT; ++n) {
       const int r = r0 + 16 * n;
