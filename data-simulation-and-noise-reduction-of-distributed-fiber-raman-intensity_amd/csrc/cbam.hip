@@ -1002,7 +1002,7 @@ enum XMode : int { XM_PROBE = 0, XM_L2 = 1, XM_SC1 = 2 };
 constexpr unsigned TAG_OFF_XCD = 0x80000000u;
 __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& ta, char* slot, unsigned* ctr,
                                           bool arrive, const h16c::ChanStats* pre, unsigned tag, int xmode,
-                                          bool local) {
+                                          bool local, Stamps& st) {
   char* lds = tl.lds;
   const Lane ln;
   const int tid = h16c::tid();
@@ -1044,7 +1044,9 @@ __device__ __forceinline__ void publish16(const h16c::Tile& tl, const TeamArgs& 
       rm[ln.rb * 64 + c] = f2ord(mx[j]);
     }
   }
+  st(14);
   __syncthreads();
+  st(15);
   // one store phase, no drain, no arrival: the statistics (wave 0: granules {f32 sum, tag} and
   // {ordered max, tag}) and the edge rows (u, f16) for the neighbours (waves 1-2: two granules per
   // 16-B sc1 store): block 0 = rows [2H - 5, 2H) (the left neighbour's rows [WB - 5, WB)), block 1 =
@@ -1421,7 +1423,7 @@ __device__ __forceinline__ void team16_spectra(char* lds, const uint8_t* blob, c
       char* mine = tslots + ((size_t)(nbar & 1) * ta.TT + tile) * SLOT16_BYTES;
       const bool skip = ta.force_miss > 0 && __builtin_amdgcn_workgroup_id_x() == 0 && nbar + 1 == (unsigned)ta.force_miss;
       st(1);
-      publish16(tl, ta, mine, ctr, !skip, pre, ta.tag0 + nbar + 1, xmode, local);
+      publish16(tl, ta, mine, ctr, !skip, pre, ta.tag0 + nbar + 1, xmode, local, st);
       st(3);
       st(4);
       apply16<EDGE>(tl, ta, tslots + (size_t)(nbar & 1) * ta.TT * SLOT16_BYTES, slot, ADS, res, id, st,

@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "data-simulation-and-noise-reduction-of-di
 
 PHASES = ["save_identity", "conv1", "conv2", "publish:atomic", "wait", "apply:pointwise", "stem/head/store",
           "loop-other", "publish:rows", "publish:barrier", "apply:slots", "apply:mlp", "apply:spatial-stats",
-          "apply:sa-conv"]
+          "apply:sa-conv", "publish16:reduce", "publish16:barrier"]
 NSTAMP = 16
 
 
