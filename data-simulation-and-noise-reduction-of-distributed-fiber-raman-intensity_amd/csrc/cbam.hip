@@ -1227,6 +1227,16 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   }
   __syncthreads();
   st(10);
+  // the spatial pass's u rows (below), fetched now: their LDS latency hides under the MLP's chain
+  constexpr int SROWS = WB16 / h16c::WAVES;    // 80 rows per wave
+  static_assert(SROWS % 16 == 0, "whole 16-row groups per wave");
+  V ua[SROWS / 16], ub[SROWS / 16];
+#pragma unroll
+  for (int k = 0; k < SROWS / 16; ++k) {
+    const int r = SROWS * w + ln.c16 + 16 * k;
+    ua[k] = *(const V*)(lds + h16c::BUF0 + h16c::soff(r, ln.q));
+    ub[k] = *(const V*)(lds + h16c::BUF0 + h16c::soff(r, ln.q + 4));
+  }
   // channel attention, evaluated whole by every wave (no barrier): the pooled avg / max of channel
   // `lane` from the 8 partials in a fixed order, the 4 + 4 hidden units as sums over the 64 lanes
   float cav;
@@ -1294,16 +1304,7 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   const V cah = ca_slot(ln.slot()), cq0 = ca_slot(ln.q), cq4 = ca_slot(ln.q + 4);
   float* m1 = (float*)(lds + M1_OFF) + 3;      // [mean_c; max_c] of rows -3 .. WB + 2, zero outside
   float* m2 = (float*)(lds + M2_OFF) + 3;      // the tile and [0, L)
-  constexpr int SROWS = WB16 / h16c::WAVES;    // 80 rows per wave
-  static_assert(SROWS % 16 == 0, "whole 16-row groups per wave");
   {
-    V ua[SROWS / 16], ub[SROWS / 16];
-#pragma unroll
-    for (int k = 0; k < SROWS / 16; ++k) {
-      const int r = SROWS * w + ln.c16 + 16 * k;
-      ua[k] = *(const V*)(lds + h16c::BUF0 + h16c::soff(r, ln.q));
-      ub[k] = *(const V*)(lds + h16c::BUF0 + h16c::soff(r, ln.q + 4));
-    }
 #pragma unroll
     for (int k = 0; k < SROWS / 16; ++k) {
       const V va = ua[k] * cq0, vb = ub[k] * cq4;
@@ -1335,6 +1336,10 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   }
   __syncthreads();
   st(12);
+  // the product pass's u rows (below), fetched now: their latency hides under conv7
+  V uv[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) uv[n] = *(const V*)(b0 + n * 16 * h16c::ROWB);
   // sa = sigmoid(conv7([mean_c; max_c]))
   float* sa = (float*)(lds + SA16_OFF);
   // two adjacent rows per thread (their 7-tap windows share 6 rows): the 320 row pairs of the tile
@@ -1360,16 +1365,12 @@ __device__ __forceinline__ void apply16(const h16c::Tile& tl, const TeamArgs& ta
   }
   __syncthreads();
   st(13);
-  V uv[NT];
   // h = [identity +] u*ca*sa [relu], in place, packed f16.  Rows at positions outside [0, L) stay zero
   // without a check: u is 0 there (conv2's zero_outside; the stem's for the first CBAM), ca and sa are
   // finite, and the identity -- the block input, an earlier h -- is 0 there too
   float sv[NT];
 #pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    uv[n] = *(const V*)(b0 + n * 16 * h16c::ROWB);
-    sv[n] = sa[ln.row(n)];
-  }
+  for (int n = 0; n < NT; ++n) sv[n] = sa[ln.row(n)];
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     V* pu = (V*)(b0 + n * 16 * h16c::ROWB);
