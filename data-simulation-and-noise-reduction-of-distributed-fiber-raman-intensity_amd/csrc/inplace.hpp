@@ -870,8 +870,13 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
       }
     }
   };
+  // (walk, a spectrum's short last tiles) block j's rows all lie 8 or more positions beyond L: no
+  // output inside [0, L) reaches them within the remaining corrected layers and the head (d = 1: 6
+  // positions), so the block skips its MFMAs, B reads and write-back (its rows keep older values,
+  // which only feed rows beyond L: never stored, never tracked by the range guard)
+  auto beyond = [&](int j) { return WALK && EDGE && tl.base + BR * j >= tl.L + 8; };
   auto store_block = [&](int j) {
-    if (j == NB - 1 && half_idle) return;
+    if ((j == NB - 1 && half_idle) || beyond(j)) return;
     if constexpr (MODE == MODE_H8) {
 #pragma unroll
       for (int i = 0; i < NT; ++i) store_pair(j, i);
@@ -892,7 +897,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   for (int i = 0; i < NT; ++i) bnext[i] = read_b(0, 0, i);
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const bool skip = j == NB - 1 && half_idle;       // no rows of this wave in the half block
+    const bool skip = (j == NB - 1 && half_idle) || beyond(j);   // no rows of this wave / none needed
     f32x4 part[SP][NT][MT];
     f32x4 hi[COMP ? NT : 1][COMP ? MT : 1];          // COMP: running total, starts at the bias
 #pragma unroll
@@ -980,7 +985,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
         }
         if (k < 2 * tl.dn_prev) *(u32x4c*)(tl.lds + tl.cs_prev + k * ROWB_F32 + 16 * sl) = carry_b;
       }
-      if (j >= 2) {
+      if (j >= 2 && !beyond(j - 2)) {
         constexpr int NP = NT * MT;
         if constexpr (MODE == MODE_H8) {
           if (s < NT) store_pair(j - 2, s);
