@@ -2,7 +2,7 @@
 # the rocprofv3 kernel trace of the same bench (the dominant kernel's average must not exceed that
 # line's ms_per_step), PMC passes (separate processes, gfx950 slot limits) for the headline hybrid,
 # plain f16, and the CBAM team kernels (ADSDN / APIDN 'f16').
-#   then, on the build host: python tools/summarize_profiles.py gpurun_out/final profiles/r04
+#   then, on the build host: python tools/summarize_profiles.py gpurun_out/final profiles/r05
 set +e
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
