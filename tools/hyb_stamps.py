@@ -66,7 +66,8 @@ def main():
     w = ws.view(torch.int64).cpu().tolist()
     n = w[1 + len(PHASES)]
     tot = sum(w[1:1 + len(PHASES)])
-    tiles = -(-(L + 28) // 512) if os.environ.get("RDN_WALK") == "1" else 1
+    wt = int(os.environ.get("RDN_WALK_ROWS_MIX", "576"))     # the walk tile of the build (common.hpp)
+    tiles = -(-(L + 28) // wt) if os.environ.get("RDN_WALK") == "1" else 1
     print(f"{e0.elapsed_time(e1) / 5:.2f} ms per forward of {B} spectra; {n} hybrid workgroups stamped; "
           f"{tot / n:.0f} cycles per workgroup ({tiles} tiles each; per tile below)")
     n *= tiles
