@@ -264,9 +264,11 @@ def time_forward(engine, arch, dtype, packed, x, y, steps, warmup, stream):
 def time_pipeline(engine, arch, dtype, packed, seed, first, B, L, steps, stream, dev):
     """SURVEY.md §8d configs 3-4 end to end, reported beside `value` (never as it): per step the
     device simulator writes B fresh spectra (indices first + i*B, i = 0..steps: the caller gives each
-    rank a disjoint block of (steps + 1) * B indices), the fused forward denoises them and the fp64
-    metric kernel accumulates the evaluate sums (evaulate.py:29-39) — no host sync, nothing leaves
-    HBM.  Also times each stage alone on the same buffers."""
+    rank a disjoint block of (steps + 1) * B indices), the fused forward denoises them and meters them
+    into the evaluate sums (evaulate.py:29-39) — no host sync, nothing leaves HBM.  The step is
+    simulate -> rdn_forward_metrics (on the walk geometry the forward kernel computes each spectrum's
+    metrics after its walk: no second pass over y); also timed: each stage alone and the unfused step
+    (simulate -> forward -> metrics kernel) on the same buffers."""
     clean = torch.empty((B, L), dtype=torch.float32, device=dev)
     noisy = torch.empty((B, L), dtype=torch.float32, device=dev)
     y = torch.empty((B, 1, L), dtype=torch.float32, device=dev)
@@ -280,6 +282,12 @@ def time_pipeline(engine, arch, dtype, packed, seed, first, B, L, steps, stream,
 
     def met():
         engine.metrics(y.view(B, L), clean, sums=sums, per_spectrum=False)
+
+    fused = []
+
+    def fwdmet():
+        fused.append(engine.forward_metrics(arch, dtype, packed, noisy.view(B, 1, L), clean, out=y, sums=sums,
+                                            check=False)[3])
 
     def timed(fn):
         fn(0)
@@ -295,12 +303,16 @@ def time_pipeline(engine, arch, dtype, packed, seed, first, B, L, steps, stream,
     ms_gen = timed(gen)
     ms_fwd = timed(lambda i: fwd())
     ms_met = timed(lambda i: met())
+    ms_fm = timed(lambda i: fwdmet())
+    ms_unfused = timed(lambda i: (gen(i), fwd(), met()))
     sums.zero_()
-    ms_all = timed(lambda i: (gen(i), fwd(), met()))
+    ms_all = timed(lambda i: (gen(i), fwdmet()))
     return {"spectra_per_s_per_gpu": B / (ms_all * 1e-3), "ms_per_step": ms_all, "batch": B, "steps": steps,
-            "stage_ms": {"simulate": ms_gen, "forward": ms_fwd, "metrics": ms_met},
+            "stage_ms": {"simulate": ms_gen, "forward": ms_fwd, "metrics": ms_met, "forward_metrics": ms_fm},
+            "metric_epilogue_fused": all(fused), "unfused_ms_per_step": ms_unfused,
             "spectra_metered": int(sums[4].item()),
-            "note": "simulate -> fused forward -> fp64 metric sums per step, all on device (configs 3-4)"}
+            "note": "simulate -> forward with the metric epilogue (rdn_forward_metrics) per step, all on device "
+                    "(configs 3-4); unfused_ms_per_step: simulate -> forward -> separate metrics kernel"}
 
 
 class ClockSampler:
@@ -351,6 +363,11 @@ def time_sustained(engine, arch, dtype, packed, seed, first, B, L, seconds, min_
     y = torch.empty((B, 1, L), dtype=torch.float32, device=dev)
     steps = max(1, -(-min_spectra // B))
     ev = lambda: torch.cuda.Event(enable_timing=True)   # noqa: E731
+    # every step's outputs count only if finite: the workspace's status word (a saturated e4m3 tile) is
+    # checked once after the window, and a device flag ANDs in each step's finiteness (no host sync)
+    ws = engine.Workspace(arch, dtype, B, L, dev) if engine.needs_workspace(arch, engine.resolve_dtype(arch, dtype)) \
+        else None
+    finite = torch.ones((), dtype=torch.bool, device=dev)
     # one untimed step (pack / launch caches), then the window
     engine.generate(B, seed, first_index=first, signal_length=L, device=dev, out=(clean, noisy))
     engine.forward(arch, dtype, packed, noisy.view(B, 1, L), out=y, check=False)
@@ -363,9 +380,10 @@ def time_sustained(engine, arch, dtype, packed, seed, first, B, L, seconds, min_
             engine.generate(B, seed, first_index=first + (i + 1) * B, signal_length=L, device=dev, out=(clean, noisy))
             a, b = ev(), ev()
             a.record(stream)
-            engine.forward(arch, dtype, packed, noisy.view(B, 1, L), out=y, check=False)
+            engine.forward(arch, dtype, packed, noisy.view(B, 1, L), out=y, check=False, workspace=ws)
             b.record(stream)
             fwd.append((a, b))
+            torch.logical_and(finite, torch.isfinite(y).all(), out=finite)
             i += 1
             if i % 16 == 0:
                 torch.cuda.synchronize()
@@ -374,7 +392,9 @@ def time_sustained(engine, arch, dtype, packed, seed, first, B, L, seconds, min_
                     break
         torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    if not bool(torch.isfinite(y).all()):
+    if ws is not None:
+        ws.check()                               # raises on a saturated tile in any step of the window
+    if not bool(finite):
         raise RuntimeError("non-finite outputs in the sustained window")
     ms_fwd = [a.elapsed_time(b) for a, b in fwd]
     kms = sum(ms_fwd) / len(ms_fwd)

@@ -24,11 +24,11 @@ hipError_t launch_fused16(int arch, const uint8_t* blob, const float* x, float* 
 hipError_t launch_fused16_f16(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
                               hipStream_t s);
 hipError_t launch_fused16_f16_walk(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
-                                   unsigned* status, hipStream_t s);
+                                   unsigned* status, const met::MetricOut* mo, hipStream_t s);
 hipError_t launch_fused16_f16_small(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
                                    unsigned* status, hipStream_t s);
 hipError_t launch_fused_inplace_walk(const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
-                                     hipStream_t s);
+                                     const met::MetricOut* mo, hipStream_t s);
 hipError_t launch_fused_inplace_short(const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
                                       hipStream_t s);
 hipError_t launch_fused_inplace(int arch, int dtype, const uint8_t* blob, const float* x, float* y, int64_t n, int L,
@@ -38,7 +38,7 @@ hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const f
                                void* ws, size_t ws_bytes, hipStream_t s);
 size_t cbam_workspace_bytes(int arch, int dtype, int64_t n, int64_t L, hipStream_t s);
 hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t s, int* timed_out,
-                       int* out_of_range);
+                       int* out_of_range, int* gate);
 hipError_t cbam_workspace_init(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t s);
 hipError_t launch_generate(uint64_t seed, uint64_t first, int64_t n, int L, float snr_lo, float snr_hi, float extreme_prob,
                            int max_repeat, float* clean, float* noisy, float* snr, float* nstd, hipStream_t s);
@@ -247,78 +247,122 @@ static bool walk_tiles(int arch, int dtype, int64_t n, int64_t L, hipStream_t s)
   return walk_rows < tile_rows;
 }
 
-int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* y, int64_t n, int64_t L, void* ws,
-                size_t ws_bytes, void* stream) {
-  RDN_GUARD_BEGIN
-  if (!valid_arch(arch) || !valid_dtype(dtype)) return fail(RDN_EINVAL, "rdn_forward: unknown arch/dtype");
-  if (!packed || !x || !y) return fail(RDN_EINVAL, "rdn_forward: null pointer");
-  if (n < 0 || L < 1 || L > 0x7fffffff) return fail(RDN_EINVAL, "rdn_forward: need n >= 0 and 1 <= L < 2^31");
+// The forward of rdn_forward / rdn_forward_metrics.  mo (may be NULL): metrics of y against mo->clean;
+// on the walk geometry the forward kernel computes them (each spectrum's workgroup after its walk,
+// *fused = true), otherwise the metrics kernel runs after the forward on the same stream.
+static int forward_impl(const char* who, int arch, int dtype, const void* packed, const float* x, float* y, int64_t n,
+                        int64_t L, void* ws, size_t ws_bytes, const rdn::met::MetricOut* mo, hipStream_t s, bool* fused) {
+  if (!valid_arch(arch) || !valid_dtype(dtype)) return fail(RDN_EINVAL, std::string(who) + ": unknown arch/dtype");
+  if (!packed || !x || !y) return fail(RDN_EINVAL, std::string(who) + ": null pointer");
+  if (n < 0 || L < 1 || L > 0x7fffffff) return fail(RDN_EINVAL, std::string(who) + ": need n >= 0 and 1 <= L < 2^31");
+  if (mo && L < 7) return fail(RDN_EINVAL, std::string(who) + ": need L >= 7 (SSIM window)");
   if (n == 0) return RDN_OK;
   {  // tiles re-read their input halos while other tiles' outputs (and parked head rows) land in y
     const uintptr_t xb = (uintptr_t)x, yb = (uintptr_t)y, bytes = (uintptr_t)(n * L) * sizeof(float);
-    if (xb < yb + bytes && yb < xb + bytes) return fail(RDN_EINVAL, "rdn_forward: x and y overlap");
+    if (xb < yb + bytes && yb < xb + bytes) return fail(RDN_EINVAL, std::string(who) + ": x and y overlap");
   }
-  if (unsupported(arch, dtype)) return fail_unsupported("rdn_forward");
-  const hipStream_t s = (hipStream_t)stream;
+  if (unsupported(arch, dtype)) return fail_unsupported(who);
   const uint8_t* blob = (const uint8_t*)packed;
+  hipError_t e = hipSuccess;
+  bool done = false;          // metrics computed by the forward kernel
   if (is_cbam(arch)) {
     const size_t need = rdn::cbam_workspace_bytes(arch, dtype, n, L, s);
     if (ws_bytes < need || (need && !ws))
-      return fail(RDN_ESIZE, "rdn_forward: workspace too small, need " + std::to_string(need) + " bytes");
-    return hip_check(rdn::launch_cbam_forward(arch, dtype, blob, x, y, n, (int)L, ws, ws_bytes, s), "cbam forward");
+      return fail(RDN_ESIZE, std::string(who) + ": workspace too small, need " + std::to_string(need) + " bytes");
+    e = rdn::launch_cbam_forward(arch, dtype, blob, x, y, n, (int)L, ws, ws_bytes, s);
+  } else {
+    // status word of the 16-bit dtypes (optional: without a workspace a saturated tile still writes NaN,
+    // and the input gate is not reported)
+    unsigned* status = status_word(dtype) && ws && ws_bytes >= RANGE_WS_BYTES ? (unsigned*)ws : nullptr;
+    const bool shrt = dtype != RDN_BF16 && short_tiles(arch, n, L, s);
+    const bool walk = dtype != RDN_BF16 && !shrt && walk_tiles(arch, dtype, n, L, s);
+    if (dtype == RDN_BF16) e = rdn::launch_fused16(arch, blob, x, y, n, (int)L, status, s);
+    else if (dtype == RDN_F16 && walk) e = rdn::launch_fused16_f16_walk(arch, blob, x, y, n, (int)L, status, mo, s), done = true;
+    else if (dtype == RDN_F16)
+      e = shrt ? rdn::launch_fused16_f16_small(arch, blob, x, y, n, (int)L, status, s)
+               : rdn::launch_fused16_f16(arch, blob, x, y, n, (int)L, status, s);
+    else if (dtype == RDN_F16MIX && walk) e = rdn::launch_fused_inplace_walk(blob, x, y, n, (int)L, status, mo, s), done = true;
+    else if (dtype == RDN_F16MIX && shrt) e = rdn::launch_fused_inplace_short(blob, x, y, n, (int)L, status, s);
+    else e = rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, status, s);
   }
-  // status word of the 16-bit dtypes (optional: without a workspace a saturated tile still writes NaN,
-  // and the input gate is not reported)
-  unsigned* status = status_word(dtype) && ws && ws_bytes >= RANGE_WS_BYTES ? (unsigned*)ws : nullptr;
-  if (dtype == RDN_BF16) return hip_check(rdn::launch_fused16(arch, blob, x, y, n, (int)L, status, s), "fused bf16 forward");
-  const bool shrt = short_tiles(arch, n, L, s);
-  const bool walk = !shrt && walk_tiles(arch, dtype, n, L, s);
-  if (dtype == RDN_F16 && walk)
-    return hip_check(rdn::launch_fused16_f16_walk(arch, blob, x, y, n, (int)L, status, s), "fused f16 forward (walk)");
-  if (dtype == RDN_F16)
-    return hip_check(shrt ? rdn::launch_fused16_f16_small(arch, blob, x, y, n, (int)L, status, s)
-                          : rdn::launch_fused16_f16(arch, blob, x, y, n, (int)L, status, s), "fused f16 forward");
-  if (dtype == RDN_F16MIX && walk)
-    return hip_check(rdn::launch_fused_inplace_walk(blob, x, y, n, (int)L, status, s), "fused f16mix forward (walk)");
-  if (dtype == RDN_F16MIX && shrt)
-    return hip_check(rdn::launch_fused_inplace_short(blob, x, y, n, (int)L, status, s), "fused f16mix forward (short tiles)");
-  return hip_check(rdn::launch_fused_inplace(arch, dtype, blob, x, y, n, (int)L, status, s), "fused in-place forward");
+  if (e != hipSuccess) return hip_check(e, who);
+  done = done && mo;
+  if (fused) *fused = done;
+  if (mo && !done) e = rdn::launch_metrics(y, mo->clean, mo->clean_f64 != 0, n, (int)L, mo->per, mo->sums, mo->acc, s);
+  return hip_check(e, who);
+}
+
+int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* y, int64_t n, int64_t L, void* ws,
+                size_t ws_bytes, void* stream) {
+  RDN_GUARD_BEGIN
+  return forward_impl("rdn_forward", arch, dtype, packed, x, y, n, L, ws, ws_bytes, nullptr, (hipStream_t)stream, nullptr);
   RDN_GUARD_END
 }
 
-int rdn_forward_status(int arch, int dtype, int64_t n, int64_t L, void* ws, size_t ws_bytes, void* stream) {
+int rdn_forward_metrics(int arch, int dtype, const void* packed, const float* x, float* y, int64_t n, int64_t L,
+                        const void* clean, int clean_is_f64, double* per_spectrum, double* sums, int64_t* acc, void* ws,
+                        size_t ws_bytes, void* stream, int* fused) {
   RDN_GUARD_BEGIN
-  if (!valid_arch(arch) || !valid_dtype(dtype)) return fail(RDN_EINVAL, "rdn_forward_status: unknown arch/dtype");
-  if (n < 0 || L < 1 || L > 0x7fffffff) return fail(RDN_EINVAL, "rdn_forward_status: bad n / L");
-  if (unsupported(arch, dtype)) return fail_unsupported("rdn_forward_status");
-  const hipStream_t s = (hipStream_t)stream;
+  if (!clean) return fail(RDN_EINVAL, "rdn_forward_metrics: null clean pointer");
+  if (clean_is_f64 != 0 && clean_is_f64 != 1) return fail(RDN_EINVAL, "rdn_forward_metrics: clean_is_f64 must be 0 or 1");
+  const rdn::met::MetricOut mo{clean, clean_is_f64, per_spectrum, sums, (long long*)acc};
+  bool f = false;
+  const int rc = forward_impl("rdn_forward_metrics", arch, dtype, packed, x, y, n, L, ws, ws_bytes, &mo, (hipStream_t)stream, &f);
+  if (fused) *fused = rc == RDN_OK && f ? 1 : 0;
+  return rc;
+  RDN_GUARD_END
+}
+
+// rdn_forward_status / rdn_forward_status_ex: wait for the stream, read and clear every sticky status
+// word, report all of them through *flags, fail on a hand-off timeout (RDN_EHIP) or a saturated
+// activation (RDN_ERANGE); the input gate is informational (flags only).
+static int forward_status(const char* who, int arch, int dtype, int64_t n, int64_t L, void* ws, size_t ws_bytes,
+                          hipStream_t s, unsigned* flags) {
+  if (flags) *flags = 0;
+  if (!valid_arch(arch) || !valid_dtype(dtype)) return fail(RDN_EINVAL, std::string(who) + ": unknown arch/dtype");
+  if (n < 0 || L < 1 || L > 0x7fffffff) return fail(RDN_EINVAL, std::string(who) + ": bad n / L");
+  if (unsupported(arch, dtype)) return fail_unsupported(who);
   if (!is_cbam(arch)) {
-    int rc = hip_check(hipStreamSynchronize(s), "rdn_forward_status");
+    int rc = hip_check(hipStreamSynchronize(s), who);
     if (rc != RDN_OK || !status_word(dtype) || !ws || ws_bytes < RANGE_WS_BYTES) return rc;
     unsigned w = 0;
-    rc = hip_check(hipMemcpy(&w, ws, sizeof(w), hipMemcpyDeviceToHost), "rdn_forward_status");
+    rc = hip_check(hipMemcpy(&w, ws, sizeof(w), hipMemcpyDeviceToHost), who);
     if (rc != RDN_OK) return rc;
     if (!w) return RDN_OK;
+    if (flags) *flags = w & (RDN_STATUS_RANGE | RDN_STATUS_GATE);
     // cleared on the forwards' stream: ordered before the next forward enqueued there
-    rc = hip_check(hipMemsetAsync(ws, 0, 4, s), "rdn_forward_status");
+    rc = hip_check(hipMemsetAsync(ws, 0, 4, s), who);
     // the input-gate bit is informational (the module's fp32 re-run decision): only the range bit fails
     return rc != RDN_OK || !(w & rdn::STATUS_RANGE) ? rc : fail(RDN_ERANGE, range_msg());
   }
-  if (n == 0) return hip_check(hipStreamSynchronize(s), "rdn_forward_status");
+  if (n == 0) return hip_check(hipStreamSynchronize(s), who);
   const size_t need = rdn::cbam_workspace_bytes(arch, dtype, n, L, s);
   if (ws_bytes < need || (need && !ws))
-    return fail(RDN_ESIZE, "rdn_forward_status: workspace smaller than this device's CBAM geometry needs (" +
+    return fail(RDN_ESIZE, std::string(who) + ": workspace smaller than this device's CBAM geometry needs (" +
                                std::to_string(need) + " bytes)");
-  int timed_out = 0, out_of_range = 0;
-  const int rc = hip_check(rdn::cbam_status(arch, dtype, L, ws, ws_bytes, s, &timed_out, &out_of_range),
-                           "rdn_forward_status");
+  int timed_out = 0, out_of_range = 0, gate = 0;
+  const int rc = hip_check(rdn::cbam_status(arch, dtype, L, ws, ws_bytes, s, &timed_out, &out_of_range, &gate), who);
   if (rc != RDN_OK) return rc;
+  if (flags)
+    *flags = (out_of_range ? RDN_STATUS_RANGE : 0u) | (gate ? RDN_STATUS_GATE : 0u) | (timed_out ? RDN_STATUS_TIMEOUT : 0u);
   if (timed_out)
     return fail(RDN_EHIP, "CBAM team hand-off timed out: a workgroup of a spectrum's team never arrived (the "
                           "grid's co-residency was broken, e.g. by a concurrent kernel on the device); the "
                           "affected spectra's outputs are NaN");
   if (out_of_range) return fail(RDN_ERANGE, range_msg());
   return RDN_OK;
+}
+
+int rdn_forward_status(int arch, int dtype, int64_t n, int64_t L, void* ws, size_t ws_bytes, void* stream) {
+  RDN_GUARD_BEGIN
+  return forward_status("rdn_forward_status", arch, dtype, n, L, ws, ws_bytes, (hipStream_t)stream, nullptr);
+  RDN_GUARD_END
+}
+
+int rdn_forward_status_ex(int arch, int dtype, int64_t n, int64_t L, void* ws, size_t ws_bytes, void* stream,
+                          unsigned* flags) {
+  RDN_GUARD_BEGIN
+  return forward_status("rdn_forward_status_ex", arch, dtype, n, L, ws, ws_bytes, (hipStream_t)stream, flags);
   RDN_GUARD_END
 }
 

@@ -54,7 +54,8 @@ struct Seg {
   float* u_out;
   double* sum_out;
   unsigned* max_out;
-  unsigned* range;              // MODE_H8 range guard words: [0] this forward, [1] sticky (cbam_status)
+  unsigned* range;              // status words: [0] MODE_H8 range, this forward; [1] range, sticky; [2] the
+                                // input gate (STATUS_GATE, raised by the first segment's stem), sticky
 };
 
 __device__ __forceinline__ unsigned f2ord(float f) {
@@ -255,8 +256,13 @@ __global__ __launch_bounds__(THREADS) void segment(const uint8_t* __restrict__ b
   LayerA<MODE> a;
   if (sg.n_convs) load_layer_a<MODE>(tl, sg.layer0, a);
   zero_guards(lds);
-  if (sg.pro == PRO_STEM) prologue_stem<MODE>(tl, sg, n);
-  else prologue_cbam<MODE>(tl, sg, n);
+  if (sg.pro == PRO_STEM) {
+    tl.status = sg.range + 2;            // the stem reads every x: the input-gate word
+    prologue_stem<MODE>(tl, sg, n);
+    tl.status = nullptr;
+  } else {
+    prologue_cbam<MODE>(tl, sg, n);
+  }
   __syncthreads();
   for (int i = 0; i < sg.n_convs; ++i) {
     const bool more = i + 1 < sg.n_convs;
@@ -343,7 +349,9 @@ struct TeamArgs {
   char* slots;          // [teams][2][TT][SLOT_BYTES]
   unsigned* counters;   // [teams][TEAM_CTR_STRIDE], zeroed before the launch
   char* hsave;          // [teams * TT][WB][64] f32
-  unsigned* err;         // hand-off error words: [0] this launch (fast-fail, NaN outputs), [1] sticky (cbam_status)
+  unsigned* err;         // status words: [0] hand-off error, this launch (fast-fail, NaN outputs); [1] hand-off
+                         // error, sticky; [2] MODE_H8 range, sticky; [3] the input gate (STATUS_GATE: the stems
+                         // read every x), sticky -- the sticky words are read and cleared by cbam_status
   unsigned long long* stamps;   // RDN_TEAM_STAMPS diagnostics: [grid][NSTAMP] cycle sums per phase
   int force_miss;       // test knob (RDN_CBAM_FORCE_MISS=k): workgroup 0 skips its k-th arrival
   int xcd;              // team16: 1 = same-XCD teams may hand off through their XCD's L2
@@ -803,7 +811,7 @@ __global__ __launch_bounds__(THREADS) void team_forward(const uint8_t* __restric
     tl.layer = 0;
     tl.corr = corr_mask(blob);
     tl.amax = 0.f;
-    tl.status = nullptr;
+    tl.status = ta.err + 3;               // the stems raise the input gate
     LayerA<MODE> a;
     load_layer_a<MODE>(tl, 0, a);
     bool tainted = false;                 // MODE_H8: a tile of this spectrum saturated (apply_cbam)
@@ -1410,6 +1418,7 @@ __device__ __forceinline__ void team16_spectra(char* lds, const uint8_t* blob, c
   team_range(ta, team, nloc, n_lo, n_hi);
   for (int64_t n = n_lo; n < n_hi; ++n) {
     h16c::Tile tl = h16c::init_tile(lds, blob, big16, x + (size_t)n * L, L, tile * ta.T - ta.halo);
+    tl.status = ta.err + 3;               // the stems raise the input gate
     h16c::Frags F0, F1;
     V id[NT];
     h16c::ChanStats cs;
@@ -1759,47 +1768,50 @@ hipError_t launch_cbam_forward(int arch, int dtype, const uint8_t* blob, const f
   return hipSuccess;
 }
 
-// A new workspace: clear the sticky status words -- the team kernel's hand-off error word and range
-// word (err[1], err[2]), or the segment path's range word (the caller checked the size).
+// A new workspace: clear the sticky status words -- the team kernel's hand-off error, range and input-
+// gate words (err[1..3]), or the segment path's range and gate words (the caller checked the size).
 hipError_t cbam_workspace_init(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t stream) {
   const TeamGeo tg = team_geo(arch, team_mode(dtype), L, stream_device(stream));
   if (tg.teams <= 0) {
     if (!ws) return hipSuccess;
-    return hipMemsetAsync(seg_range(ws), 0, 8, stream);
+    return hipMemsetAsync(seg_range(ws), 0, 12, stream);
   }
   if (!ws || ws_bytes < tg.total) return hipErrorInvalidValue;
-  return hipMemsetAsync(team_err(tg, ws) + 1, 0, 8, stream);          // the sticky words
+  return hipMemsetAsync(team_err(tg, ws) + 1, 0, 12, stream);         // the sticky words
 }
 
 // After CBAM forwards on `stream`: wait for them, then read and clear the sticky status words.
 // *timed_out = 1 if a team wait of any forward since the last read exceeded its spin limit (outputs
-// of affected spectra are NaN); *out_of_range = 1 if a MODE_H8 activation saturated.  The caller
-// checked the workspace size.
+// of affected spectra are NaN); *out_of_range = 1 if a MODE_H8 activation saturated; *gate = 1 if an
+// input left [-INPUT_GATE, INPUT_GATE].  The caller checked the workspace size.
 hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes, hipStream_t stream,
-                       int* timed_out, int* out_of_range) {
+                       int* timed_out, int* out_of_range, int* gate) {
   *timed_out = 0;
   *out_of_range = 0;
+  *gate = 0;
   hipError_t e = hipStreamSynchronize(stream);
   if (e != hipSuccess) return e;
   const TeamGeo tg = team_geo(arch, team_mode(dtype), L, stream_device(stream));
   unsigned* words;
   if (tg.teams <= 0) {
     if (!ws) return hipSuccess;
-    words = seg_range(ws);                                              // [0] forward, [1] sticky
+    words = seg_range(ws);                                              // [1] range, [2] gate (sticky)
   } else {
     if (!ws || ws_bytes < tg.total) return hipErrorInvalidValue;
-    words = team_err(tg, ws);                                           // [1] timeout, [2] range (sticky)
+    words = team_err(tg, ws);                                           // [1] timeout, [2] range, [3] gate
   }
-  unsigned w[3] = {0, 0, 0};
+  unsigned w[4] = {0, 0, 0, 0};
   e = hipMemcpy(w, words, sizeof(w), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return e;
   if (tg.teams <= 0) {
     *out_of_range = w[1] != 0;
-    if (w[1]) e = hipMemsetAsync(words + 1, 0, 4, stream);     // on the forwards' stream (ordered)
+    *gate = w[2] != 0;
+    if (w[1] || w[2]) e = hipMemsetAsync(words + 1, 0, 8, stream);     // on the forwards' stream (ordered)
   } else {
     *timed_out = w[1] != 0;
     *out_of_range = w[2] != 0;
-    if (w[1] || w[2]) e = hipMemsetAsync(words + 1, 0, 8, stream);
+    *gate = w[3] != 0;
+    if (w[1] || w[2] || w[3]) e = hipMemsetAsync(words + 1, 0, 12, stream);
   }
   return e;
 }

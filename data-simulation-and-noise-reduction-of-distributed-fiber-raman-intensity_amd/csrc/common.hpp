@@ -99,6 +99,21 @@ __device__ __forceinline__ void raise_status(unsigned* status, unsigned bit) {
   __hip_atomic_fetch_or(status, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Static issue priority of one half of a 512-thread workgroup (MI355X_MICROARCH.md "Two waves per SIMD"
+// item 4: waves w and w + 4 share a SIMD, and the second-dispatched half loses the VALU / LDS issue
+// arbitration to the first at equal priority).  RDN_SETPRIO = 1: waves 4-7 at priority 1; 2: waves 0-3;
+// 0: none.  Set once at kernel entry, never flipped.
+#ifndef RDN_SETPRIO
+#define RDN_SETPRIO 0
+#endif
+__device__ __forceinline__ void wave_priority() {
+#if RDN_SETPRIO == 1
+  if (__builtin_amdgcn_readfirstlane(__builtin_amdgcn_workitem_id_x() >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
+#elif RDN_SETPRIO == 2
+  if (__builtin_amdgcn_readfirstlane(__builtin_amdgcn_workitem_id_x() >> 6) < 4) __builtin_amdgcn_s_setprio(1);
+#endif
+}
+
 // 16-bit single-rounding layout of fused16.hip (RDN_BF16, non-CBAM networks): the same
 // [m 4][kstep 6][lane 64][8] fragments + bias, but with the K order permuted so that element j of
 // lane quarter q in k-step (t, u) is cin = h16_channel(4u + q, j) — the channel held by element j
@@ -153,6 +168,25 @@ __host__ __device__ constexpr int walk_shift(int arch) {
 __host__ __device__ constexpr int fused_halo(int arch) {
   return arch == DENOISECNN ? 20 : arch == RRCDNET ? 29 : arch == DSDN ? 34 : arch == PIDN ? 32 : 0;
 }
+
+namespace met {
+// where a launch's metric results go (any pointer may be NULL; clean == NULL: no metrics): the
+// standalone metrics kernel and the walk kernels' metric epilogue (metrics.hpp)
+struct MetricOut {
+  const void* clean;     // fp32 or fp64 [n][L], the clean reference of each spectrum
+  int clean_f64;
+  double* per;           // fp64 [n][4] per-spectrum values
+  double* sums;          // fp64 [5] accumulated {sum MSE, SSIM, Smoothness, Peak2Peak, count}
+  long long* acc;        // exact accumulator, RDN_ACC_WORDS int64 (accumulated)
+};
+// the outputs of a launch chunk starting at spectrum n0 (no metrics: clean = NULL)
+inline MetricOut chunk(const MetricOut* mo, int64_t n0, int L) {
+  if (!mo || !mo->clean) return MetricOut{nullptr, 0, nullptr, nullptr, nullptr};
+  const size_t es = mo->clean_f64 ? 8 : 4;
+  return MetricOut{(const char*)mo->clean + (size_t)n0 * L * es, mo->clean_f64, mo->per ? mo->per + n0 * 4 : nullptr,
+                   mo->sums, mo->acc};
+}
+}  // namespace met
 
 struct Geometry {       // tiling of one launch
   int L;                // spectrum length

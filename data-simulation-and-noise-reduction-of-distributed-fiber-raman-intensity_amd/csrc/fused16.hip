@@ -3,6 +3,7 @@
 // DSDN/train.py:72-126, PIDN/train.py:72-106.
 #include "fused16.hpp"
 #include "host_util.hpp"
+#include "metrics.hpp"
 
 namespace rdn {
 
@@ -292,8 +293,10 @@ __device__ __forceinline__ void dsdn_tile(Tile& tl, float* y, int t, int ntiles,
 #define H16_WALK_KERNEL(name, SHIFT, C0)                                                                   \
   __global__ __launch_bounds__(THREADS) void name##_walk(const uint8_t* __restrict__ blob,                 \
                                                          const float* __restrict__ x, float* __restrict__ y, \
-                                                         int L, int ntiles, unsigned* __restrict__ status) { \
+                                                         int L, int ntiles, unsigned* __restrict__ status, \
+                                                         met::MetricOut mo) {                               \
     extern __shared__ __attribute__((aligned(16))) char lds[];                                             \
+    wave_priority();                                                                                       \
     const int n = __builtin_amdgcn_workgroup_id_x();                                                       \
     Tile tl = init_tile(lds, blob, blob + SMALL_BYTES, x + (size_t)n * L, L, 0);                           \
     tl.status = status;                                                                                    \
@@ -306,6 +309,7 @@ __device__ __forceinline__ void dsdn_tile(Tile& tl, float* y, int t, int ntiles,
       else name##_tile<false>(tl, y, t, ntiles, F0, F1, xs);                                               \
       tl.first = false;                                                                                    \
     }                                                                                                      \
+    if (mo.clean) met::walk_metrics(y, L, n, lds, mo);  /* the metric epilogue: y read back from L2 */    \
   }
 
 H16_WALK_KERNEL(denoisecnn, DENOISECNN_SHIFT, 0)
@@ -315,12 +319,13 @@ H16_WALK_KERNEL(dsdn, DSDN_SHIFT, 0)
 
 }  // namespace H16_NS
 
-typedef void (*walk_kernel_t)(const uint8_t*, const float*, float*, int, int, unsigned*);
+typedef void (*walk_kernel_t)(const uint8_t*, const float*, float*, int, int, unsigned*, met::MetricOut);
 
 // Host launcher: one workgroup per spectrum (the grid should hold many spectra per CU: a spectrum is
-// one CU's sequential walk); ntiles = ceil((L + head shift) / WT).
+// one CU's sequential walk); ntiles = ceil((L + head shift) / WT).  mo (may be NULL): the metric
+// epilogue's outputs (metrics.hpp walk_metrics), computed by each spectrum's workgroup after its walk.
 hipError_t H16_LAUNCH(int arch, const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
-                      hipStream_t stream) {
+                      const met::MetricOut* mo, hipStream_t stream) {
   walk_kernel_t k = nullptr;
   int shift = 0;
   switch (arch) {
@@ -336,7 +341,7 @@ hipError_t H16_LAUNCH(int arch, const uint8_t* blob, const float* x, float* y, i
   for (int64_t n0 = 0; n0 < n; n0 += 0x7fffffff) {
     const int64_t nn = n - n0 < 0x7fffffff ? n - n0 : 0x7fffffff;
     hipLaunchKernelGGL(k, dim3((unsigned)nn), dim3(H16_NS::THREADS), H16_NS::LDS_BYTES, stream, blob, x + n0 * L,
-                       y + n0 * L, L, ntiles, status);
+                       y + n0 * L, L, ntiles, status, met::chunk(mo, n0, L));
   }
   return hipGetLastError();
 }

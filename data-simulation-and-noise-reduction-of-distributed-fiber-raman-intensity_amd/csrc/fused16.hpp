@@ -98,6 +98,12 @@ constexpr int BIAS_OFF = H16_BIAS_OFF;
 #ifndef RDN_H16_PF
 #define RDN_H16_PF 3
 #endif
+#ifndef RDN_H16_ESPLIT
+#define RDN_H16_ESPLIT 0
+#endif
+#ifndef RDN_H16_SGB
+#define RDN_H16_SGB 0
+#endif
 // A tile holding positions outside [0, L) stores its layer outputs unmasked (the MFMA loop is the
 // interior tiles' own) and each wave then zeroes its rows outside [0, L) -- a few stores after the
 // loop, before the barrier (zero_outside; a per-lane range check and select in every epilogue made
@@ -589,6 +595,10 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   Acc prev;
   constexpr int PF = RDN_H16_PF;       // B fragments in flight ahead of the step that consumes them
   constexpr int K = KS * NT;           // steps (N-tile n, k-step s), k = KS n + s
+  // RDN_H16_ESPLIT = e > 1 (f16 RELU / LINEAR layers): the previous N-tile's rounding and ReLU at step
+  // 1, its ds_write_b128 at step e, so one step no longer carries the whole epilogue (diagnostic A/B)
+  constexpr bool ESPLIT = RDN_H16_ESPLIT > 1 && RDN_H16_F16 && (EPI == RELU || EPI == LINEAR);
+  V pend;
   V B[PF + 1];
 #pragma unroll
   for (int k = 0; k < PF; ++k) B[k] = *(const V*)(tl.lds + ba.at(k / KS, k % KS));
@@ -607,12 +617,31 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
         if (n > 0 && s == 0) idn[n & 1] = *(const V*)(tl.lds + sid + n * NR * ROWB);
       }
       mstep(F, s, B[k % (PF + 1)], acc);
-      if (n > 0 && s == 1) epilogue(n - 1, prev);
+      if constexpr (ESPLIT) {
+        if (n > 0 && s == 1) {
+          V hv = __builtin_convertvector(__builtin_shufflevector(prev.v[0], prev.v[1], 0, 1, 2, 3, 4, 5, 6, 7), V);
+          if (EPI == RELU) hv = __builtin_elementwise_max(hv, (V)((E)0));
+          pend = hv;
+        }
+        if (n > 0 && s == RDN_H16_ESPLIT) *(V*)(tl.lds + sa + (n - 1) * NR * ROWB) = pend;
+      } else {
+        if (n > 0 && s == 1) epilogue(n - 1, prev);
+      }
       if (WALK && n == 1 && s == 0) carry_store(tl, dst, CA, cc, CROW);
 #if !defined(RDN_ABLATE_NOALOAD)
       // the next layer's operands, one buffer load every LDSTEP-th step: the vector-memory traffic
       // of the CU's 8 waves spreads over the layer
       if (has_next && k % LDSTEP == 0 && k / LDSTEP < NLOAD) load_op(tl, next, h, k / LDSTEP, lo, G);
+#endif
+#if RDN_H16_SGB
+      // explicit interleave inside the step (diagnostic A/B): MFMA, VALU, B read, MFMA, VALU, store, load
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, RDN_H16_SGB, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
 #endif
       __builtin_amdgcn_sched_barrier(0);
     }

@@ -5,6 +5,7 @@
 // PIDN/train.py:72-106.
 #include "inplace.hpp"
 #include "host_util.hpp"
+#include "metrics.hpp"
 // the f16 ping-pong layers of fused16.hpp over the f16 + e4m3 blob (its leading f16 fragments):
 // the plain layers of RDN_F16MIX (rrcdnet_hybrid below)
 #define RDN_H16_F16 1
@@ -328,13 +329,10 @@ __device__ __forceinline__ bool spectrum_outside(char* lds, const float* xs, int
 // RDN_F16MIX RRCDNet on the walk geometry: one workgroup per spectrum (rrcdnet_hybrid_walk.hpp); a
 // spectrum with a spike takes the tiled hybrid tile by tile (T, tiles: the 640-row geometry)
 template <int TAIL>
-__global__ __launch_bounds__(THREADS) void rrcdnet_hybrid_walk(const uint8_t* __restrict__ blob,
-                                                               const float* __restrict__ x, float* __restrict__ y,
-                                                               int L, int T, int tiles, int ntiles,
-                                                               unsigned* __restrict__ status) {
+__device__ __forceinline__ void hybrid_walk_spectrum(char* lds, const uint8_t* __restrict__ blob,
+                                                     const float* __restrict__ x, float* __restrict__ y, int L, int T,
+                                                     int tiles, int ntiles, unsigned* __restrict__ status, int n) {
   static_assert(TAIL == F16MIX_TAIL, "the walk body is written for the compiled-in tail");
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int n = __builtin_amdgcn_workgroup_id_x();
   if (!f16mix_blob_ok(blob)) {
     for (int p = __builtin_amdgcn_workitem_id_x(); p < L; p += THREADS) y[(size_t)n * L + p] = __uint_as_float(0x7fc00000u);
     return;
@@ -367,6 +365,36 @@ __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid_walk(const uint8_t* __
   for (; t < ntiles && (t + 1) * hybw::PP::WT <= L; ++t) hybw::tile<false>(tl, t16, y, t, ntiles, F0, F1, xs, status, st);
   for (; t < ntiles; ++t) hybw::tile<true>(tl, t16, y, t, ntiles, F0, F1, xs, status, st);
   st.flush(status);
+}
+// MET: the spectrum's metrics follow its walk in the same workgroup (metrics.hpp walk_metrics; a
+// separate instantiation, so the plain forward's register allocation does not see the epilogue).  The
+// epilogue reads y and mo from the kernel-argument segment after the walk (an opaque pointer, so the
+// loads are not hoisted to the kernel's start): held in SGPRs across the walk, they cost 44 more
+// spilled VGPRs in the tile loop.  HybWalkArgs mirrors the parameter list (the kernarg layout).
+struct HybWalkArgs {
+  const uint8_t* blob;
+  const float* x;
+  float* y;
+  int L, T, tiles, ntiles;
+  unsigned* status;
+  met::MetricOut mo;
+};
+template <int TAIL, bool MET>
+__global__ __launch_bounds__(THREADS) void rrcdnet_hybrid_walk(const uint8_t* __restrict__ blob,
+                                                               const float* __restrict__ x, float* __restrict__ y,
+                                                               int L, int T, int tiles, int ntiles,
+                                                               unsigned* __restrict__ status, met::MetricOut mo) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  wave_priority();
+  const int n = __builtin_amdgcn_workgroup_id_x();
+  hybrid_walk_spectrum<TAIL>(lds, blob, x, y, L, T, tiles, ntiles, status, n);
+  if (MET) {
+    __syncthreads();                   // the walk's (or the spiked fallback's) last LDS use is done
+    const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    const HybWalkArgs* a = (const HybWalkArgs*)ka;
+    met::walk_metrics(a->y + (size_t)n * a->L, a->L, n, lds, a->mo);
+  }
 }
 
 // RDN_F16MIX RRCDNet on 256-row tiles (the hybrid body on h16xs + the 2-block in-place tile): the
@@ -444,16 +472,18 @@ hipError_t launch_fused_inplace_short(const uint8_t* blob, const float* x, float
 
 // RDN_F16MIX RRCDNet on the walk geometry (ip::rrcdnet_hybrid_walk): one workgroup per spectrum
 hipError_t launch_fused_inplace_walk(const uint8_t* blob, const float* x, float* y, int64_t n, int L, unsigned* status,
-                                     hipStream_t stream) {
-  const auto k = ip::rrcdnet_hybrid_walk<ip::RRCDNET_F16MIX_TAIL>;
-  const hipError_t e = ensure_dynamic_lds((const void*)k, 93, 163840, stream_device(stream));
+                                     const met::MetricOut* mo, hipStream_t stream) {
+  const bool met = mo && mo->clean;
+  const auto k = met ? ip::rrcdnet_hybrid_walk<ip::RRCDNET_F16MIX_TAIL, true> : ip::rrcdnet_hybrid_walk<ip::RRCDNET_F16MIX_TAIL, false>;
+  // attribute slots 93 / 94, host_util.hpp
+  const hipError_t e = ensure_dynamic_lds((const void*)k, met ? 94 : 93, 163840, stream_device(stream));
   if (e != hipSuccess) return e;
   const int H = fused_halo(RRCDNET), T = ip::TileGeo<5>::WB - 2 * H, tiles = (L + T - 1) / T;
   const int ntiles = (int)(((int64_t)L + walk_shift(RRCDNET) + RDN_WALK_ROWS_MIX - 1) / RDN_WALK_ROWS_MIX);
   for (int64_t n0 = 0; n0 < n; n0 += 0x7fffffff) {
     const int64_t nn = n - n0 < 0x7fffffff ? n - n0 : 0x7fffffff;
     hipLaunchKernelGGL(k, dim3((unsigned)nn), dim3(THREADS), 163840, stream, blob, x + n0 * L, y + n0 * L, L, T, tiles,
-                       ntiles, status);
+                       ntiles, status, met::chunk(mo, n0, L));
   }
   return hipGetLastError();
 }

@@ -47,6 +47,9 @@ template <int NBK> struct TileGeo {
 // layer's input, taps r - 2d, r - d, r: nothing is read past the computed rows), no wrap.
 // WB = RDN_WALK_ROWS_MIX computed rows in NBK blocks; when WB = 128 NBK - 64 the last block is half
 // (HALF): its rows are those of the waves of quarters nq = 0, 1, and the waves of quarters 2, 3 skip it.
+#ifndef RDN_HALF_REMAP
+#define RDN_HALF_REMAP 0
+#endif
 template <int NBK> struct WalkGeo {
   static constexpr int WB = RDN_WALK_ROWS_MIX;
   static constexpr bool HALF = WB == 128 * NBK - 64;
@@ -738,8 +741,16 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   uint32_t sc_l[MT];
 #pragma unroll
   for (int mm = 0; mm < MT; ++mm) bias_l[mm] = a.bias[mm], sc_l[mm] = a.sc[mm];
-  // WalkGeo HALF: the waves of quarters 2, 3 have no rows in the last block (wave-uniform)
-  const bool half_idle = TG::HALF && (__builtin_amdgcn_readfirstlane(tid >> 6) >> 1) >= 2;
+  // WalkGeo HALF: the last block holds 64 rows.  RDN_HALF_REMAP = 0: the waves of quarters 2, 3 have no
+  // rows there (wave-uniform) and the others run their two N-tiles; RDN_HALF_REMAP = 1: every wave runs
+  // ONE N-tile of it, rows 16 nq + [0, 16) (its usual B / store addresses moved by -16 nq rows, a multiple
+  // of 16: same swizzle, one address add per access), so the half block costs half a block
+  constexpr bool REMAP = TG::HALF && RDN_HALF_REMAP;
+  static_assert(!REMAP || MODE == MODE_H8, "the half-block remap is written for the f16 + e4m3 write-back");
+  const bool half_idle = TG::HALF && !REMAP && (__builtin_amdgcn_readfirstlane(tid >> 6) >> 1) >= 2;
+  const uint32_t hoff = REMAP ? (uint32_t)(16 * ROWB_F32) * (uint32_t)__builtin_amdgcn_readfirstlane(nq) : 0u;
+  // the remapped block's rows of this wave start 16 nq, not 32 nq, rows into it
+  auto remapped = [&](int j) { return REMAP && j == NB - 1; };
   typedef unsigned int u32x4c __attribute__((ext_vector_type(4)));
   u32x4c carry_a = {0u, 0u, 0u, 0u}, carry_b = {0u, 0u, 0u, 0u};
   const bool cwave = WALK && __builtin_amdgcn_readfirstlane(tid >> 6) == THREADS / 64 - 1;
@@ -796,6 +807,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   auto read_b = [&](int j, int s, int i) -> typename O::B {
     if (TG::WRAP && j == 0 && s < TS && i == 0) return ldb(bfirst[s], 0);
     if (TG::WRAP && j == NB - 1 && s >= 2 * TS && i == NT - 1) return ldb(blast[s - 2 * TS], 0);
+    if (remapped(j)) return ldb(j >= 2 ? badr2[s] : badr[s], (uint32_t)(BR * (j >= 2 ? j - 2 : j)) * ROWB_F32 - hoff);
     if (j >= 2) return ldb(badr2[s], (uint32_t)(BR * (j - 2) + 16 * i) * ROWB_F32);
     return ldb(badr[s], (uint32_t)(BR * j + 16 * i) * ROWB_F32);
   };
@@ -829,8 +841,8 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   // stores instead of 6); ReLU folded into the saturating med3
   auto store_pair = [&](int j, int i) {
     if constexpr (MODE == MODE_H8) {                // (instantiated in every mode, called in MODE_H8)
-      const int rb = BR * j + (BR / 4) * nq;
-      const bool inside = !EDGE || (tl.base + rb >= 0 && tl.base + rb + BR / 4 <= tl.L);
+      const int rb = BR * j + (remapped(j) ? 16 : BR / 4) * nq;
+      const bool inside = !EDGE || (tl.base + rb >= 0 && tl.base + rb + (remapped(j) ? 16 : BR / 4) <= tl.L);
       const bool zero = !inside && !in_range(tl.base + rb + 16 * i + c16, tl.L);
       if (!cout) {                 // plain f16 output (the next layer is uncorrected): no e4m3 planes
         f16x4 hv[MT];
@@ -843,7 +855,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
           if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
           hv[mm] = __builtin_convertvector(v, f16x4);
         }
-        *(f16x8*)(tl.lds + sadr[0][0] + (uint32_t)(BR * j + 16 * i) * ROWB_F32) =
+        *(f16x8*)(tl.lds + sadr[0][0] + (uint32_t)(BR * j + 16 * i) * ROWB_F32 - (remapped(j) ? hoff : 0u)) =
             __builtin_shufflevector(hv[0], hv[1], 0, 1, 2, 3, 4, 5, 6, 7);
         return;
       }
@@ -858,7 +870,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
         if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
         x[mm] = h8_split(v);
       }
-      const uint32_t off = (uint32_t)(BR * j + 16 * i) * ROWB_F32;
+      const uint32_t off = (uint32_t)(BR * j + 16 * i) * ROWB_F32 - (remapped(j) ? hoff : 0u);
       typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   #if defined(RDN_ABLATE_NOSTORE)
       if (x[0].hi8 == 0x12345678u)
@@ -879,7 +891,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
     if ((j == NB - 1 && half_idle) || beyond(j)) return;
     if constexpr (MODE == MODE_H8) {
 #pragma unroll
-      for (int i = 0; i < NT; ++i) store_pair(j, i);
+      for (int i = 0; i < (remapped(j) ? 1 : NT); ++i) store_pair(j, i);
     } else {
 #pragma unroll
       for (int i = 0; i < NT; ++i)
@@ -924,7 +936,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
     for (int s = 0; s < O::KSTEPS; ++s) {
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
-        if (!skip) {
+        if (!skip && !(remapped(j) && i > 0)) {
 #pragma unroll
         for (int mm = 0; mm < MT; ++mm) {
           if constexpr (MODE == MODE_H8 && !(EPI & (ADD_ID | SAVE_ID))) {
@@ -949,7 +961,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
           }
         }
         if (s + 1 < O::KSTEPS) bnext[i] = read_b(j, s + 1, i);
-        else if (j + 1 < NB && !(j + 1 == NB - 1 && half_idle)) bnext[i] = read_b(j + 1, 0, i);
+        else if (j + 1 < NB && !(j + 1 == NB - 1 && half_idle) && !(remapped(j + 1) && i > 0)) bnext[i] = read_b(j + 1, 0, i);
         }
         if constexpr (COMP) {
           // fold a finished chunk into the running totals (the rounding error becomes the next

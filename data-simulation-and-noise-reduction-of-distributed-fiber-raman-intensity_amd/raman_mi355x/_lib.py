@@ -18,7 +18,7 @@ CSRC = os.path.join(os.path.dirname(PKG), "csrc")
 HEADER = os.path.join(os.path.dirname(os.path.dirname(PKG)), "include", "raman_mi355x.h")
 
 RDN_OK = 0
-ABI_VERSION = 5
+ABI_VERSION = 6
 # exact metric accumulator words (include/raman_mi355x.h RDN_ACC_*)
 ACC_LIMBS = 6
 ACC_STRIDE = ACC_LIMBS + 1
@@ -70,6 +70,12 @@ _SIGNATURES = {
     "rdn_check_blob": ([ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t], ctypes.c_int),
     "rdn_forward": ([ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                      ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
+    "rdn_forward_metrics": ([ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                             ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "rdn_forward_status_ex": ([ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                               ctypes.c_size_t, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint)], ctypes.c_int),
     "rdn_generate": ([ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, ctypes.POINTER(GenParams), ctypes.c_void_p,
                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "rdn_metrics": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,

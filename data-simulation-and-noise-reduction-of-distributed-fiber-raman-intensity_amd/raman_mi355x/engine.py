@@ -20,7 +20,7 @@ RANGE_CODES = (3, 5)
 # a fused network's 16-bit forward keeps a status word in its workspace (common.hpp STATUS_*): bit 0 an
 # e4m3 activation saturated (RANGE_CODES only), bit 1 an input left [-4, 4] (the stems' input gate,
 # models.INPUT_GATE: the 16-bit modes' domain; informational, rdn_forward_status does not fail on it)
-STATUS_RANGE, STATUS_GATE = 1, 2
+STATUS_RANGE, STATUS_GATE, STATUS_TIMEOUT = 1, 2, 4
 # Engine arithmetic modes (include/raman_mi355x.h rdn_dtype).  Every name here except
 # "bf16-unsafe" meets its north-star tolerance on every golden fixture (fp32: 1e-5 max-relative;
 # 16-bit modes: 2e-2 max-abs).  Single-rounding bf16 does NOT (0.24 on trained RRCDNet),
@@ -243,9 +243,37 @@ class Workspace:
             return int(self.status_word().item())
 
     def check(self):
-        """Wait for the stream; raise if a CBAM hand-off of any forward since the last check timed out."""
-        _lib.check(_lib.lib().rdn_forward_status(self.arch, self.code, self.n, self.L, self.ptr, self.bytes,
-                                                 ctypes.c_void_p(self.stream.cuda_stream)), "rdn_forward_status")
+        """Wait for the stream, read and clear the status words of every forward since the last check, and
+        return their flags (STATUS_RANGE | STATUS_GATE | STATUS_TIMEOUT, rdn_forward_status_ex).  Raises
+        EngineError if a CBAM hand-off timed out, RangeError if a tile saturated the e4m3 planes; the
+        input gate (an input beyond the 16-bit modes' domain) is only reported in the flags."""
+        flags = ctypes.c_uint(0)
+        _lib.check(_lib.lib().rdn_forward_status_ex(self.arch, self.code, self.n, self.L, self.ptr, self.bytes,
+                                                    ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(flags)),
+                   "rdn_forward_status_ex")
+        return int(flags.value)
+
+
+def _forward_args(arch, dtype, x, out, check, workspace, _ws_checked):
+    """Shared argument checks of forward / forward_metrics: (n, L, arch id, code, y, workspace)."""
+    _check_cuda_f32(x, "input")
+    if x.dim() == 3 and x.shape[1] != 1:
+        raise ValueError(f"expected (N, 1, L) input, got {tuple(x.shape)}")
+    if x.dim() not in (2, 3):
+        raise ValueError(f"expected (N, 1, L) input, got {tuple(x.shape)}")
+    n, L = x.shape[0], x.shape[-1]
+    a, code = _arch(arch), resolve_dtype(arch, dtype)
+    y = torch.empty_like(x) if out is None else out
+    if out is not None:
+        _check_out(y, "out", x.shape, x.device)
+    if y.data_ptr() < x.data_ptr() + x.numel() * 4 and x.data_ptr() < y.data_ptr() + y.numel() * 4:
+        raise ValueError("out must not overlap the input (tiles re-read input halos while outputs are written)")
+    ws = workspace
+    if ws is None and (a in CBAM_IDS or (check and code in RANGE_CODES)):
+        ws = Workspace(a, code, n, L, x.device)
+    elif ws is not None and not _ws_checked and not ws.fits(a, code, n, L, x.device):
+        raise ValueError("workspace was made for another network, dtype, length, device, stream or a smaller batch")
+    return n, L, a, code, y, ws
 
 
 def forward(arch, dtype, packed, x, out=None, check=True, workspace=None, _ws_checked=False):
@@ -266,23 +294,8 @@ def forward(arch, dtype, packed, x, out=None, check=True, workspace=None, _ws_ch
     co-resident teams hold) NaNs every spectrum of the chunk.  The status word (RangeError from
     ``check`` or ``Workspace.check()``) remains the authoritative signal."""
     _check_cuda_f32(x, "input")
-    if x.dim() == 3 and x.shape[1] != 1:
-        raise ValueError(f"expected (N, 1, L) input, got {tuple(x.shape)}")
-    if x.dim() not in (2, 3):
-        raise ValueError(f"expected (N, 1, L) input, got {tuple(x.shape)}")
     x = x.contiguous()
-    n, L = x.shape[0], x.shape[-1]
-    a, code = _arch(arch), resolve_dtype(arch, dtype)
-    y = torch.empty_like(x) if out is None else out
-    if out is not None:
-        _check_out(y, "out", x.shape, x.device)
-    if y.data_ptr() < x.data_ptr() + x.numel() * 4 and x.data_ptr() < y.data_ptr() + y.numel() * 4:
-        raise ValueError("out must not overlap the input (tiles re-read input halos while outputs are written)")
-    ws = workspace
-    if ws is None and (a in CBAM_IDS or (check and code in RANGE_CODES)):
-        ws = Workspace(a, code, n, L, x.device)
-    elif ws is not None and not _ws_checked and not ws.fits(a, code, n, L, x.device):
-        raise ValueError("workspace was made for another network, dtype, length, device, stream or a smaller batch")
+    n, L, a, code, y, ws = _forward_args(arch, dtype, x, out, check, workspace, _ws_checked)
     L_ = _lib.lib()
     _lib.check(L_.rdn_forward(a, code, ctypes.c_void_p(packed.data_ptr()), ctypes.c_void_p(x.data_ptr()),
                               ctypes.c_void_p(y.data_ptr()), n, L,
@@ -291,6 +304,45 @@ def forward(arch, dtype, packed, x, out=None, check=True, workspace=None, _ws_ch
     if check and ws is not None:
         ws.check()
     return y
+
+
+def forward_metrics(arch, dtype, packed, x, clean, out=None, sums=None, per_spectrum=False, acc=None, check=True,
+                    workspace=None):
+    """forward() and metrics() in one call (rdn_forward_metrics): y = Model(x), then each spectrum's MSE,
+    SSIM, Smoothness and Peak2Peak against ``clean`` (float32 or float64, (N, L) or (N, 1, L)), added to
+    ``sums`` / ``acc`` as metrics() does.  On the walk geometry (large batches of the f16 modes) the
+    forward kernel computes the metrics itself after each spectrum's walk, so y is not read again by a
+    second pass.  Returns (y, per (n, 4) or None, sums, fused)."""
+    _check_cuda_f32(x, "input")
+    x = x.contiguous()
+    if not (torch.is_tensor(clean) and clean.is_cuda):
+        raise RuntimeError("raman_mi355x runs on the GPU only: clean must be a CUDA (HIP) tensor")
+    if clean.dtype not in (torch.float32, torch.float64):
+        raise TypeError(f"clean must be float32 or float64, got {clean.dtype}")
+    n, L, a, code, y, ws = _forward_args(arch, dtype, x, out, check, workspace, False)
+    clean = clean.reshape(clean.shape[0], -1).contiguous()
+    if tuple(clean.shape) != (n, L):
+        raise ValueError(f"clean must be ({n}, {L}), got {tuple(clean.shape)}")
+    if clean.device != x.device:
+        raise ValueError(f"input on {x.device} but clean on {clean.device}")
+    per = torch.empty((n, 4), dtype=torch.float64, device=x.device) if per_spectrum else None
+    if sums is None:
+        sums = torch.zeros(5, dtype=torch.float64, device=x.device)
+    else:
+        _check_out(sums, "sums", (5,), x.device, torch.float64)
+    if acc is not None:
+        _check_out(acc, "acc", (_lib.ACC_WORDS,), x.device, torch.int64)
+    fused = ctypes.c_int(0)
+    _lib.check(_lib.lib().rdn_forward_metrics(
+        a, code, ctypes.c_void_p(packed.data_ptr()), ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), n, L,
+        ctypes.c_void_p(clean.data_ptr()), int(clean.dtype == torch.float64),
+        ctypes.c_void_p(per.data_ptr() if per is not None else 0), ctypes.c_void_p(sums.data_ptr()),
+        ctypes.c_void_p(acc.data_ptr() if acc is not None else 0),
+        ws.ptr if ws is not None else ctypes.c_void_p(0), ws.bytes if ws is not None else 0, _stream(x.device),
+        ctypes.byref(fused)), "rdn_forward_metrics")
+    if check and ws is not None:
+        ws.check()
+    return y, per, sums, bool(fused.value)
 
 
 def generate(n, seed, first_index=0, signal_length=10000, snr_range=(20.0, 37.0), extreme_noise_prob=0.05,

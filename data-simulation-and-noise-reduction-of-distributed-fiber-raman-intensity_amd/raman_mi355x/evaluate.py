@@ -64,39 +64,14 @@ def _engine_module(model):
     return isinstance(model, _EngineNet) and type(model).forward is _EngineNet.forward
 
 
-def _model_forward(model, x, ws):
-    """The module's forward without the per-call hand-off check (one Workspace.check at the end);
-    any other nn.Module (or an engine module whose input the engine does not take) runs model(x), as
-    evaulate.py:30 does."""
-    if not (_engine_module(model) and model.uses_engine(x)):
-        return model(x)
-    return engine.forward(model.ARCH, model.engine_code, model.packed_weights(x.device), x, check=False,
-                          workspace=ws)
-
-
-def _gate(model, device):
-    """Device running max of |input| for a CBAM engine module in a 16-bit mode (models.INPUT_GATE); the
-    fused networks' kernels raise the input-gate bit of their workspace's status word instead (_gate_hit)."""
-    if not _engine_module(model) or model.engine_code == 0 or engine.has_status_word(model.ARCH, model.engine_code):
-        return None
-    return torch.zeros((), dtype=torch.float32, device=device)
-
-
-def _gate_hit(ws):
-    """Whether a fused network's forwards since the workspace's last check saw an input beyond the gate."""
-    return ws is not None and bool(ws.read_status() & engine.STATUS_GATE)
-
-
-def _track(gate, x):
-    lo, hi = torch.aminmax(x)                      # one pass, no |x| copy
-    torch.maximum(gate, torch.maximum(-lo, hi), out=gate)
-
-
-def _check_gate(model, gate, hit=False):
+def _finish(model, ws):
+    """One status read after all of a network's batches (rdn_forward_status_ex: the sticky words of every
+    forward since): raises on a timed-out CBAM hand-off or a saturated tile, and RangeError when a 16-bit
+    forward saw an input beyond the gate (the kernels' stems raise it, fused and CBAM networks alike)."""
     from .models import INPUT_GATE
-    if hit or (gate is not None and float(gate) > INPUT_GATE):
-        seen = "" if gate is None else f" (reached {float(gate):.3g})"
-        raise _lib.RangeError(f"evaluate: |input| beyond the 16-bit modes' domain{seen} ({INPUT_GATE}, normalised "
+    flags = ws.check() if ws is not None else 0
+    if flags & engine.STATUS_GATE and model.engine_code != 0:
+        raise _lib.RangeError(f"evaluate: |input| beyond the 16-bit modes' domain ({INPUT_GATE}, normalised "
                               f"intensity); evaluate this data in 'fp32'")
 
 
@@ -130,20 +105,19 @@ def evaluate(model, noisy_data, clean_data, batch_size=1024, device=None):
     # fp64 clean stays fp64 (the metrics compare against the same float64 values as evaulate.py)
     cdt = torch.float64 if (clean.dtype == torch.float64 if torch.is_tensor(clean) else clean.dtype == np.float64) \
         else torch.float32
-    gate = _gate(model, device)
     with torch.no_grad():
         for b0 in range(lo, hi, batch_size):
             b1 = min(hi, b0 + batch_size)
             x = torch.as_tensor(noisy[b0:b1], dtype=torch.float32).to(device).unsqueeze(1)
             c = torch.as_tensor(clean[b0:b1], dtype=cdt).to(device)
-            y = _model_forward(model, x, ws)
-            if gate is not None and model.uses_engine(x):
-                _track(gate, x)
-            engine.metrics(y.squeeze(1), c, per_spectrum=False, acc=acc)
-    hit = _gate_hit(ws)
-    if ws is not None:
-        ws.check()
-    _check_gate(model, gate, hit)
+            if _engine_module(model) and model.uses_engine(x):
+                # the engine's forward + metric sums (fused into the forward kernel on the walk geometry)
+                engine.forward_metrics(model.ARCH, model.engine_code, model.packed_weights(x.device), x, c, acc=acc,
+                                       check=False, workspace=ws)
+            else:
+                y = model(x)
+                engine.metrics(y.squeeze(1), c, per_spectrum=False, acc=acc)
+    _finish(model, ws)
     _all_reduce_acc(acc)
     return means_from_acc(acc)
 
@@ -174,7 +148,6 @@ def evaluate_synthetic(models, total, seed=20250410, signal_length=10000, batch_
             model.eval()
             acc = engine.new_acc(device)
             ws = _workspace(model, B, L, device)
-            gate = _gate(model, device)
             packed = model.packed_weights(device)
             if dist.is_available() and dist.is_initialized():
                 dist.barrier()
@@ -191,15 +164,11 @@ def evaluate_synthetic(models, total, seed=20250410, signal_length=10000, batch_
                 nb = min(B, hi - b0)
                 engine.generate(nb, seed, first_index=first_index + b0, signal_length=L, device=device,
                                 out=(clean[:nb], noisy[:nb]), **gen_kwargs)
-                engine.forward(model.ARCH, model.engine_code, packed, noisy[:nb].view(nb, 1, L), out=y[:nb],
-                               check=False, workspace=ws)
-                if gate is not None:
-                    _track(gate, noisy[:nb])
-                engine.metrics(y[:nb].view(nb, L), clean[:nb], per_spectrum=False, acc=acc)
-            hit = _gate_hit(ws)
-            if ws is not None:
-                ws.check()                  # waits for the stream; raises on a timed-out hand-off / range
-            _check_gate(model, gate, hit)
+                # forward + metric sums in one call: on the walk geometry the forward kernel meters each
+                # spectrum itself (no second pass over y); otherwise the metrics kernel follows it
+                engine.forward_metrics(model.ARCH, model.engine_code, packed, noisy[:nb].view(nb, 1, L), clean[:nb],
+                                       out=y[:nb], acc=acc, check=False, workspace=ws)
+            _finish(model, ws)              # waits for the stream; raises on a timed-out hand-off / range / gate
             torch.cuda.synchronize(device)
             el = time.perf_counter() - t0
             t = torch.tensor([el], dtype=torch.float64)

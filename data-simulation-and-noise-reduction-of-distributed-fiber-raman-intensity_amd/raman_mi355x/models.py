@@ -147,11 +147,12 @@ class _EngineNet(nn.Module):
         return self._fp32[1]
 
     def _workspace(self, x):
-        """The cached status workspace of a 16-bit forward on a fused network (256 bytes, one layout:
-        the range and input-gate bits).  None otherwise: a CBAM network's team workspace depends on the
-        device geometry and the segment switch, so engine.forward makes one per call (caching allocator)."""
+        """The cached workspace of a forward: a fused network's 16-bit status word (256 bytes: the range
+        and input-gate bits), or a CBAM network's team / segment workspace (every dtype; its status words
+        hold the hand-off error, range and input-gate bits, ABI v6), re-made when the batch, length, device
+        or stream no longer fits it.  None for a fused network in fp32 (no bound to report)."""
         code = self._engine_code
-        if not engine.has_status_word(self.ARCH, code):
+        if not engine.needs_workspace(self.ARCH, code):
             return None
         n, L = x.shape[0], x.shape[-1]
         if self._ws is None or not self._ws.fits(self.ARCH, code, n, L, x.device):
@@ -181,9 +182,12 @@ class _EngineNet(nn.Module):
         ws = self._workspace(x)
         range_why = "activations beyond the e4m3 planes' range (|v| > 1792)"
         gate_why = f"|input| beyond {INPUT_GATE} (outside normalised intensity)"
+        cbam = engine.ARCH_ID[self.ARCH] in engine.CBAM_IDS
+        flags = 0
         try:
-            # a fused network's status word is read below (the call's one 4-byte host read); the CBAM
-            # networks check their own workspace inside engine.forward.  With a blob packed earlier for
+            # a fused network's status word is read below (the call's one 4-byte host read); a CBAM
+            # network's status words are read and cleared by one rdn_forward_status_ex call (its input
+            # gate included: no aminmax pass, no second sync).  With a blob packed earlier for
             # this device and dtype, a fused network launches first and checks the pack cache after
             # (a key over every parameter and buffer: ~15 us of host time, evaulate.py's batch-1 loop
             # calls this per spectrum), so the check runs while the kernel does; weights changed since
@@ -196,21 +200,21 @@ class _EngineNet(nn.Module):
             if spec and self._state_key(dev) != self._packed_key:
                 y = engine.forward(self.ARCH, code, self.packed_weights(dev), x, out=y, check=False, workspace=ws,
                                    _ws_checked=True)
+            if cbam:
+                flags = ws.check()            # waits; raises on a timed-out hand-off (EngineError) or RangeError
         except _lib.RangeError:
             # an activation left the e4m3 planes' range: never return the NaN tiles
             why = range_why
         if why is None and code != 0 and x.numel():
-            if ws is not None:
+            if not cbam and ws is not None:
                 # the kernels' stems raise the input-gate bit (they read every x), the corrected
                 # layers the range bit: no extra kernel, one wait
                 w = int(ws.status_word().item())
                 if w:
                     ws.clear_status_word()
                     why = range_why if w & engine.STATUS_RANGE else gate_why
-            else:
-                lo, hi = torch.aminmax(x)                     # CBAM networks: one pass, no |x| copy
-                if float(torch.maximum(-lo, hi)) > INPUT_GATE:
-                    why = gate_why
+            elif flags & engine.STATUS_GATE:                  # CBAM networks: the stems raised the gate
+                why = gate_why
         if why is None:
             return y
         # the batch is re-run in exact fp32, which has neither bound

@@ -22,6 +22,9 @@
  *   rdn_metrics / rdn_metrics_ex / rdn_acc_value
  *       -> compute_mse / compute_smoothness / compute_peak_to_peak + skimage SSIM, averaged
  *                                                                  <model>/evaulate.py:14-39
+ *   rdn_forward_metrics
+ *       -> the body of evaluate(): model(input) then the four metrics of each spectrum, averaged
+ *                                                                  <model>/evaulate.py:25-39
  */
 #ifndef RAMAN_MI355X_H
 #define RAMAN_MI355X_H
@@ -33,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RDN_ABI_VERSION 5
+#define RDN_ABI_VERSION 6
 
 typedef enum {
   RDN_DENOISECNN = 0, /* 1DCNN/train.py   class DenoiseCNN */
@@ -139,11 +142,14 @@ int rdn_get_correction_mask(int arch, int dtype, const void* host_blob, size_t b
  * e4m3 planes' range (the tile's outputs are NaN; rdn_forward_status returns RDN_ERANGE);
  * RDN_STATUS_GATE an input value left [-4, 4], the 16-bit modes' domain (normalised intensity: every
  * simulated spectrum lies in [-1, 2]) -- set by the kernels' stems, which read every input anyway;
- * informational (rdn_forward_status does not fail on it): the Python module reads the word once per
- * call and re-runs such a batch in RDN_F32.  Without the workspace a saturated tile still writes NaN,
- * but neither bit is reported. */
+ * informational (rdn_forward_status does not fail on it; rdn_forward_status_ex reports it): the Python
+ * module reads the word once per call and re-runs such a batch in RDN_F32.  Without the workspace a
+ * saturated tile still writes NaN, but neither bit is reported.  The CBAM networks' workspaces hold the
+ * same information in words of their own (the team kernels' and segment kernels' stems raise the gate
+ * there too, ABI v6); read it with rdn_forward_status_ex. */
 #define RDN_STATUS_RANGE 1u
 #define RDN_STATUS_GATE 2u
+#define RDN_STATUS_TIMEOUT 4u   /* rdn_forward_status_ex only: a CBAM team hand-off timed out */
 int rdn_workspace_size(int arch, int dtype, int64_t n, int64_t L, size_t* bytes, void* stream);
 
 /* Prepare a newly allocated workspace for rdn_forward on `stream`: clears its status words -- the
@@ -172,7 +178,26 @@ int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* 
  * drivers once at the end. */
 int rdn_forward_status(int arch, int dtype, int64_t n, int64_t L, void* workspace, size_t workspace_bytes,
                        void* stream);
+/* rdn_forward_status that also reports WHICH status words were set (ABI v6): *flags (may be NULL)
+ * receives RDN_STATUS_RANGE | RDN_STATUS_GATE | RDN_STATUS_TIMEOUT as read before the words were
+ * cleared, so a caller learns of the input gate (informational: no error code) without reading the
+ * workspace itself.  rdn_forward_status clears the same words and drops the gate bit: a C caller that
+ * needs it calls this form.  Every network keeps the gate: the fused networks' status word, and the
+ * CBAM networks' team / segment workspaces (their stems raise it, ABI v6). */
+int rdn_forward_status_ex(int arch, int dtype, int64_t n, int64_t L, void* workspace, size_t workspace_bytes,
+                          void* stream, unsigned* flags);
 
+/* rdn_forward followed by rdn_metrics_ex(y, clean, ...) on the same stream (ABI v6): y = Model(x), then
+ * each spectrum's MSE, SSIM, Smoothness and Peak2Peak against clean (fp32 or fp64 [n][L], device) into
+ * per_spectrum / sums / acc (each may be NULL; sums and acc ACCUMULATED, as rdn_metrics_ex).  Where the
+ * forward runs on the walk geometry (RDN_F16 on DenoiseCNN / RRCDNet / DSDN / PIDN, RDN_F16MIX on
+ * RRCDNet, large batches) the forward kernel computes them itself -- each spectrum's workgroup right
+ * after its walk, from the y rows it just wrote (read back from L2) -- so the separate metrics pass over
+ * y is gone; *fused (may be NULL) is then 1.  Otherwise the metrics kernel follows the forward (*fused
+ * = 0).  Both paths give every spectrum the same bits (one shared fp64 routine).  L must be >= 7. */
+int rdn_forward_metrics(int arch, int dtype, const void* packed, const float* x, float* y, int64_t n, int64_t L,
+                        const void* clean, int clean_is_f64, double* per_spectrum, double* sums, int64_t* acc,
+                        void* workspace, size_t workspace_bytes, void* stream, int* fused);
 /* Simulator parameters; defaults of 数据集产生.py:5-7 are {10000, 20, 37, 0.05, 40}. */
 typedef struct {
   int64_t signal_length;

@@ -6,7 +6,7 @@
 set +e
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-OUT=gpurun_out/final
+OUT=${OUT:-gpurun_out/final}
 mkdir -p $OUT
 STAGES=${STAGES:-bench kt pmc}
 if [[ " $STAGES " == *" bench "* ]]; then

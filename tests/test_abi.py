@@ -27,7 +27,7 @@ def test_exports_every_declared_symbol(lib):
     assert declared == set(_lib.EXPORTED), declared ^ set(_lib.EXPORTED)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.rdn_version() == 5
+    assert lib.rdn_version() == 6
 
 
 def test_library_built_from_these_sources(lib):

@@ -104,3 +104,60 @@ def test_metrics_clean_f64_and_exact_sums():
         exact = sum((abs(Fraction(float(v))) * 2 ** 128).__floor__() * (1 if v >= 0 else -1) for v in p[:, k])
         assert got[k] == float(Fraction(exact, 2 ** 128)), k
     assert got[4] == 9
+
+
+@pytest.mark.parametrize("walk", ["1", "0"])
+@pytest.mark.parametrize("arch,dtype", [("RRCDNet", "f16"), ("RRCDNet", "f16-plain"), ("DenoiseCNN", "f16"),
+                                        ("PIDN", "f16"), ("DSDN", "f16"), ("ADSDN", "f16"), ("RRCDNet", "fp32")])
+def test_forward_metrics_equals_forward_then_metrics(arch, dtype, walk, monkeypatch):
+    """rdn_forward_metrics (the metric epilogue, */evaulate.py:25-39): on the walk geometry (RDN_WALK=1,
+    the f16 modes of the walk networks) the forward kernel meters each spectrum itself; elsewhere the
+    metrics kernel follows the forward.  Either way y and every spectrum's four values are the bits of
+    rdn_forward followed by rdn_metrics_ex (one shared fp64 routine), for fp32 and fp64 clean, and the
+    exact accumulators are equal."""
+    from raman_mi355x import engine
+    monkeypatch.setenv("RDN_WALK", walk)
+    monkeypatch.setenv("RDN_SHORT_TILES", "0")
+    m = _model(arch, dtype)
+    dev = torch.device("cuda")
+    packed = m.packed_weights(dev)
+    n, L = 5, 2345
+    clean, noisy, _, _ = engine.generate(n, SEED, first_index=777, signal_length=L, device=dev)
+    x = noisy.view(n, 1, L)
+    walks = walk == "1" and arch in ("RRCDNet", "DenoiseCNN", "PIDN", "DSDN") and dtype != "fp32"
+    for c in (clean, clean.double()):
+        y0 = engine.forward(arch, m.engine_code, packed, x)
+        acc0 = engine.new_acc(dev)
+        per0, sums0 = engine.metrics(y0.view(n, L), c, acc=acc0)
+        acc1 = engine.new_acc(dev)
+        y1, per1, sums1, fused = engine.forward_metrics(arch, m.engine_code, packed, x, c, per_spectrum=True, acc=acc1)
+        assert fused == walks
+        assert torch.equal(y0, y1)
+        assert torch.equal(per0, per1)
+        assert torch.equal(acc0, acc1)
+        np.testing.assert_allclose(sums1.cpu().numpy(), sums0.cpu().numpy(), rtol=1e-14)
+        assert sums1[4].item() == n
+
+
+def test_forward_metrics_spiked_spectra_take_the_epilogue(monkeypatch):
+    """The RDN_F16MIX walk's spiked spectra (the tiled hybrid, tile by tile, inside the walk kernel) are
+    metered by the same epilogue: a batch of spiked and clean spectra meters all of them, and the values
+    equal the standalone metrics kernel's."""
+    from raman_mi355x import engine
+    monkeypatch.setenv("RDN_WALK", "1")
+    monkeypatch.setenv("RDN_SHORT_TILES", "0")
+    m = _model("RRCDNet", "f16")
+    dev = torch.device("cuda")
+    n, L = 6, 3000
+    clean, noisy, _, _ = engine.generate(n, SEED, first_index=4242, signal_length=L, device=dev)
+    noisy[1, 100:140] += 1.0                     # spikes: outside [-0.3, 1.3]
+    noisy[4, 2900:2950] -= 0.9
+    x = noisy.view(n, 1, L)
+    y0 = engine.forward("RRCDNet", m.engine_code, m.packed_weights(dev), x)
+    per0, _ = engine.metrics(y0.view(n, L), clean)
+    y1, per1, sums1, fused = engine.forward_metrics("RRCDNet", m.engine_code, m.packed_weights(dev), x, clean,
+                                                    per_spectrum=True)
+    assert fused
+    assert torch.equal(y0, y1)
+    assert torch.equal(per0, per1)
+    assert sums1[4].item() == n

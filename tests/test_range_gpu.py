@@ -242,3 +242,53 @@ def test_cbam_saturation_taints_whole_spectrum(arch, inputs):
     x1 = torch.from_numpy(base[1:2].astype(np.float32)).unsqueeze(1).cuda()
     y1 = engine.forward(arch, code, packed, x1, check=True).squeeze(1).cpu().numpy()
     assert np.array_equal(y1[0], y[1]), arch
+
+
+@pytest.mark.parametrize("arch,dtype", [("RRCDNet", "f16"), ("DSDN", "f16"), ("ADSDN", "f16"), ("APIDN", "f16"),
+                                        ("ADSDN", "f16f8"), ("APIDN", "bf16x3")])
+def test_status_ex_reports_input_gate(arch, dtype, inputs):
+    """rdn_forward_status_ex (ABI v6) reports the input gate of every network -- the fused networks' status
+    word and the CBAM team workspaces alike (their stems raise it): set for an input beyond [-4, 4], not
+    for normalised intensity, cleared by the read; rdn_forward_status fails on neither."""
+    import raman_mi355x as R
+    from raman_mi355x import engine
+    m = R.MODELS[arch]()
+    m.load_state_dict(golden_state_dict(arch, "trained"), strict=True)
+    m = m.cuda().eval().set_engine_dtype(dtype)
+    code = m.engine_code
+    x = inputs["main_noisy"][:2]
+    for scale, want in ((1.0, 0), (5.0, engine.STATUS_GATE), (1.0, 0)):
+        xs = torch.from_numpy((x * scale).astype(np.float32)).unsqueeze(1).cuda()
+        ws = engine.Workspace(arch, code, xs.shape[0], xs.shape[-1], xs.device)
+        engine.forward(arch, code, m.packed_weights(xs.device), xs, check=False, workspace=ws)
+        flags = ws.check()
+        assert flags & engine.STATUS_GATE == want, (arch, dtype, scale, flags)
+        assert not flags & engine.STATUS_TIMEOUT
+        assert ws.check() == 0                                   # read and cleared
+
+
+@pytest.mark.parametrize("arch", ["ADSDN", "APIDN"])
+def test_cbam_module_gate_without_host_pass(arch, inputs, monkeypatch):
+    """The CBAM networks' batch-1 module path takes the input gate from the team workspace's status words
+    (no aminmax pass over x): a spectrum beyond the gate re-runs in fp32 with one warning, one inside it
+    stays 'f16' and equals the engine's 'f16' forward bit for bit."""
+    import raman_mi355x as R
+    from raman_mi355x import engine
+
+    def no_aminmax(*a, **k):
+        raise AssertionError("the module must not scan x on the host side")
+    monkeypatch.setattr(torch, "aminmax", no_aminmax)
+    m = R.MODELS[arch]()
+    m.load_state_dict(golden_state_dict(arch, "trained"), strict=True)
+    m = m.cuda().eval().set_engine_dtype("f16")
+    x = torch.from_numpy(inputs["main_noisy"][:1].astype(np.float32)).unsqueeze(1).cuda()
+    with torch.no_grad(), warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always", RuntimeWarning)
+        y = m(x)
+        assert not w
+        ref = engine.forward(arch, m.engine_code, m.packed_weights(x.device), x)
+        assert torch.equal(y, ref)
+        y5 = m(x * 5.0)
+        assert any("ran in fp32" in str(r.message) for r in w)
+        ref5 = engine.forward(arch, 0, m._fp32_weights(x.device), x * 5.0)
+        assert torch.equal(y5, ref5)

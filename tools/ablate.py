@@ -22,7 +22,10 @@ VARIANTS = {"base": "", "prev": "", "cur": "", "cur2": "", "nolds": "-DRDN_ABLAT
             "h16f16": "-DRDN_H16_F16=1", "ld2": "-DRDN_H16_LDSTEP=2", "ld3": "-DRDN_H16_LDSTEP=3", "ld4": "-DRDN_H16_LDSTEP=4", "pf2": "-DRDN_H16_PF=2", "pf4": "-DRDN_H16_PF=4", "alledge": "-DRDN_ABLATE_ALLEDGE -DRDN_TEAM_STAMPS=1",
             "tail3": "-DRDN_F16MIX_TAIL=3", "tail4": "-DRDN_F16MIX_TAIL=4", "tail5": "-DRDN_F16MIX_TAIL=5", "nowin": "-DRDN_F16MIX_WIN=0", "nostem": "-DRDN_ABLATE_NOSTEM",
             "tail0": "-DRDN_F16MIX_TAIL=0", "tail2": "-DRDN_F16MIX_TAIL=2", "hybstamps": "-DRDN_HYB_STAMPS=1",
-            "w512": "-DRDN_WALK_ROWS=512", "w448": "-DRDN_WALK_ROWS=448", "mix512": "-DRDN_WALK_ROWS_MIX=512", "mhead": "", "lbar": "", "stg": "", "vote": "", "comb": "", "track": "", "trk2": "", "sdpp": "", "cur": "", "resplain": "", "rescomp0": "-DRDN_F32_COMP_RES=0", "reschunk6": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=6", "reschunk3": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=3", "reschunk4": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=4", "reschunk2": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=2", "nozero": "-DRDN_ABLATE_NOZERO", "nozst": "-DRDN_ABLATE_NOZERO -DRDN_TEAM_STAMPS=1", "estag": "-DRDN_H16_ESTAG=1"}
+            "w512": "-DRDN_WALK_ROWS=512", "w448": "-DRDN_WALK_ROWS=448", "mix512": "-DRDN_WALK_ROWS_MIX=512", "mhead": "", "lbar": "", "stg": "", "vote": "", "comb": "", "track": "", "trk2": "", "sdpp": "", "cur": "", "resplain": "", "rescomp0": "-DRDN_F32_COMP_RES=0", "reschunk6": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=6", "reschunk3": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=3", "reschunk4": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=4", "reschunk2": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=2", "nozero": "-DRDN_ABLATE_NOZERO", "nozst": "-DRDN_ABLATE_NOZERO -DRDN_TEAM_STAMPS=1", "estag": "-DRDN_H16_ESTAG=1",
+            "prio": "-DRDN_SETPRIO=1", "prio2": "-DRDN_SETPRIO=2", "es3": "-DRDN_H16_ESPLIT=3", "es5": "-DRDN_H16_ESPLIT=5",
+            "sgb2": "-DRDN_H16_SGB=2", "sgb4": "-DRDN_H16_SGB=4", "remap": "-DRDN_HALF_REMAP=1",
+            "prioremap": "-DRDN_SETPRIO=1 -DRDN_HALF_REMAP=1"}
 
 
 def build():
