@@ -229,7 +229,8 @@ static bool short_tiles(int arch, int64_t n, int64_t L, hipStream_t s) {
 }
 
 // Walk geometry (one workgroup walks a whole spectrum, no halo recompute: fused16_walk.hip for RDN_F16
-// on DenoiseCNN / RRCDNet, 576-row tiles; rrcdnet_hybrid_walk.hpp for RDN_F16MIX, 512-row tiles) when
+// on DenoiseCNN / RRCDNet / DSDN / PIDN -- the networks with a walk_shift -- in 576-row tiles;
+// rrcdnet_hybrid_walk.hpp for RDN_F16MIX RRCDNet, 576-row tiles, RDN_WALK_ROWS_MIX) when
 // its predicted time -- rounds of the CUs x tiles per spectrum x rows per tile -- is below that of the
 // 640-row tiles (rounds x 640 rows): large batches.  RDN_WALK = 0 / 1 forces either geometry (tests
 // compare the two).

@@ -1,5 +1,6 @@
 // RDN_F16MIX RRCDNet hybrid on the walk geometry (included once by fused_inplace.hip, namespace hybw):
-// one workgroup walks a spectrum's 512-position tiles left to right (fused16.hpp "Walk instantiation"),
+// one workgroup walks a spectrum's 576-position tiles (RDN_WALK_ROWS_MIX) left to right (fused16.hpp "Walk
+// instantiation"),
 // no halo rows recomputed.  Per tile, as the tiled hybrid (rrcdnet_hybrid.hpp): the right stem and
 // layers 0-8 on the ping-pong walk engine (h16xw), layer 9 staged into the in-place tile's three
 // planes, the corrected tail (layers 10-14) and the MFMA right head on the in-place walk engine
@@ -7,6 +8,12 @@
 // and the combine x - (r + l)/2.  Each layer's carry rows live in a slot behind the tile (128-B rows
 // for the ping-pong layers' outputs, 256-B plane rows for the outputs the corrected layers and the
 // right head read): 12,032 B.
+//
+// Range guard: tl.amax (the corrected layers' running max, inplace.hpp h8_track) is reset once per
+// spectrum, not per tile, so the first tile whose activations saturate NaNs its own outputs and those
+// of every later tile of the spectrum: the clamped values reach the next tile through its carry rows,
+// so none of its outputs could be trusted (tests/test_range_gpu.py test_walk_saturation_nans_rest_of_
+// spectrum).  The 640-row tiles, which carry nothing, NaN only the saturated tile.
 //
 // Spectra with an input outside [F16MIX_WIN_LO, F16MIX_WIN_HI] (a spike) take the tiled hybrid for
 // every tile of the spectrum instead (rrcdnet_hybrid_tile: its per-tile spiked fallback corrects every

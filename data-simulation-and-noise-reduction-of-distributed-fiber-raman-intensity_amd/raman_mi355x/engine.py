@@ -5,6 +5,7 @@ check shapes/devices, allocate outputs through the PyTorch caching allocator and
 pointers.  Nothing here has a CPU or PyTorch-op fallback.
 """
 import ctypes
+import os
 
 import torch
 
@@ -200,6 +201,7 @@ class Workspace:
         _lib.check(lib_.rdn_workspace_size(self.arch, self.code, self.n, self.L, ctypes.byref(sz), sp),
                    "rdn_workspace_size")
         self.bytes = sz.value
+        self._fit_memo = {}
         self.buf = torch.empty(self.bytes, dtype=torch.uint8, device=self.device) if self.bytes else None
         _lib.check(lib_.rdn_workspace_init(self.arch, self.code, self.n, self.L, self.ptr, self.bytes, sp),
                    "rdn_workspace_init")
@@ -212,9 +214,20 @@ class Workspace:
         """Made for this network, dtype, length and device, large enough for n spectra, and bound to the
         stream the forward launches on (torch's current stream): check() waits for self.stream only, and
         rdn_workspace_init's reset is ordered on it."""
-        return (self.arch, self.code, self.L, self.device) == (_arch(arch), code, int(L), torch.device(device)) \
-            and torch.cuda.current_stream(self.device).cuda_stream == self.stream.cuda_stream \
-            and (self.n >= n or self.bytes_for(n) <= self.bytes)
+        if not ((self.arch, self.code, self.L, self.device) == (_arch(arch), code, int(L), torch.device(device))
+                and torch.cuda.current_stream(self.device).cuda_stream == self.stream.cuda_stream):
+            return False
+        if self.arch in CBAM_IDS:
+            # the CBAM layout (team or segment geometry) is the one the device and environment give now:
+            # the size it had when made, and room for n spectra (memoised per batch size and the
+            # RDN_CBAM_SEGMENTS switch: the batch-1 loop asks once per call)
+            key = (int(n), os.environ.get("RDN_CBAM_SEGMENTS"))
+            ok = self._fit_memo.get(key)
+            if ok is None:
+                ok = self.bytes_for(self.n) == self.bytes and self.bytes_for(n) <= self.bytes
+                self._fit_memo[key] = ok
+            return ok
+        return self.n >= n or self.bytes_for(n) <= self.bytes
 
     def bytes_for(self, n):
         sz = ctypes.c_size_t()
@@ -291,8 +304,10 @@ def forward(arch, dtype, packed, x, out=None, check=True, workspace=None, _ws_ch
     statistics reach the other tiles of its spectrum through the team hand-off, so the whole spectrum
     is NaN, not just the tile: the team kernel's saturated tile publishes +inf maxima that taint its
     team (cbam.hip publish_stats / apply_cbam), and a segment-path launch (spectra longer than the
-    co-resident teams hold) NaNs every spectrum of the chunk.  The status word (RangeError from
-    ``check`` or ``Workspace.check()``) remains the authoritative signal."""
+    co-resident teams hold) NaNs every spectrum of the chunk.  On the walk geometry (large 'f16' batches
+    of RRCDNet) a saturated tile NaNs the rest of its spectrum, since its clamped values reach the next
+    tiles through the carried rows.  The status word (RangeError from ``check`` or
+    ``Workspace.check()``) remains the authoritative signal."""
     _check_cuda_f32(x, "input")
     x = x.contiguous()
     n, L, a, code, y, ws = _forward_args(arch, dtype, x, out, check, workspace, _ws_checked)

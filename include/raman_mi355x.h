@@ -73,7 +73,9 @@ typedef enum {
  *              layers of the right branch (the ones the head's cancellation x - (r + l)/2 amplifies),
  *              and every layer corrected on a tile whose input window leaves [-0.3, 1.3] (a spike):
  *              within 2e-2 (1.19e-2 on the trained fixture, 1.54e-2 worst over config 1's 1000
- *              spectra).  The corrected layers have RDN_F16F8's range and range guard (RDN_ERANGE).
+ *              spectra).  The corrected layers have RDN_F16F8's range and range guard (RDN_ERANGE);
+ *              on the walk geometry a saturated tile NaNs the rest of its spectrum (its clamped values
+ *              travel on in the carried rows), on the tile geometries the tile alone.
  *              One hybrid kernel: the plain layers, the whole left branch and its head
  *              on the RDN_F16 ping-pong engine, the corrected tail and the right head on the in-place
  *              tile.  The corrected layers are compiled in; rdn_get_correction_mask reads them back

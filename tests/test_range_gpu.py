@@ -292,3 +292,51 @@ def test_cbam_module_gate_without_host_pass(arch, inputs, monkeypatch):
         assert any("ran in fp32" in str(r.message) for r in w)
         ref5 = engine.forward(arch, 0, m._fp32_weights(x.device), x * 5.0)
         assert torch.equal(y5, ref5)
+
+
+def test_walk_saturation_nans_rest_of_spectrum(monkeypatch):
+    """The RDN_F16MIX walk (one workgroup per spectrum, carries across tiles): a tile whose activations
+    leave the e4m3 planes' range NaNs its outputs AND every later tile of the spectrum -- the clamped
+    values travel on in the carry rows, so no later tile of that spectrum may report finite outputs.
+    Spectra that stay in range are untouched, the status word reports RDN_ERANGE, and the module re-runs
+    the batch in fp32.  Inputs stay inside the spike window [-0.3, 1.3] (so the walk, not the tiled
+    fallback, runs); the right branch's convs are scaled up so the activations grow along the spectrum."""
+    import raman_mi355x as R
+    from raman_mi355x import _lib, engine
+    monkeypatch.setenv("RDN_WALK", "1")
+    monkeypatch.setenv("RDN_SHORT_TILES", "0")
+    sd = {k: v.clone() for k, v in golden_state_dict("RRCDNet", "synth").items()}
+    for k in sd:
+        if k.startswith("right_net.") and k.endswith(".0.weight") and sd[k].shape[1] == 64:
+            sd[k] *= 1.55          # CPU fp32: spectrum 1 first exceeds 1792 at position 3113, 2 at 0
+    m = R.RRCDNet()
+    m.load_state_dict(sd, strict=True)
+    m = m.cuda().eval().set_engine_dtype("f16")
+    n, L = 4, 6000
+    p = np.arange(L, dtype=np.float32) / L
+    x = np.zeros((n, L), np.float32)
+    x[0] = 0.05 * np.sin(p * 40)                      # small: stays in range (max |v| 548)
+    x[1] = 1.25 * p                                   # ramp: saturates part-way along
+    x[2] = 1.25 * p[::-1]                             # ramp down: saturates from the first tiles
+    x[3] = 0.5 + 0.0 * p                              # stays in range (max |v| 1532)
+    xs = torch.from_numpy(x).unsqueeze(1).cuda()
+    ws = engine.Workspace("RRCDNet", m.engine_code, n, L, xs.device)
+    y = engine.forward("RRCDNet", m.engine_code, m.packed_weights(xs.device), xs, check=False,
+                       workspace=ws).squeeze(1).cpu().numpy()
+    with pytest.raises(_lib.RangeError):
+        ws.check()
+    bad = np.isnan(y)
+    assert bad.any(), "the scaled weights must saturate some tile"
+    for i in range(n):
+        if bad[i].any():
+            first = int(np.argmax(bad[i]))
+            assert bad[i, first:].all(), f"spectrum {i}: finite outputs after a saturated tile"
+        print(f"spectrum {i}: NaN from {int(np.argmax(bad[i])) if bad[i].any() else None}")
+    assert not bad[0].any() and not bad[3].any()
+    first1 = int(np.argmax(bad[1]))
+    assert bad[1].any() and 0 < first1 < L, first1          # a finite prefix, then NaN to the end
+    assert bad[2].any()
+    with torch.no_grad(), warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always", RuntimeWarning)
+        ym = m(xs)
+    assert torch.isfinite(ym).all() and any("ran in fp32" in str(r.message) for r in w)
