@@ -324,10 +324,11 @@ static int forward_status(const char* who, int arch, int dtype, int64_t n, int64
   if (n < 0 || L < 1 || L > 0x7fffffff) return fail(RDN_EINVAL, std::string(who) + ": bad n / L");
   if (unsupported(arch, dtype)) return fail_unsupported(who);
   if (!is_cbam(arch)) {
-    int rc = hip_check(hipStreamSynchronize(s), who);
-    if (rc != RDN_OK || !status_word(dtype) || !ws || ws_bytes < RANGE_WS_BYTES) return rc;
+    if (!status_word(dtype) || !ws || ws_bytes < RANGE_WS_BYTES) return hip_check(hipStreamSynchronize(s), who);
+    // the word's copy is ordered behind the forwards on their stream: one wait covers both
     unsigned w = 0;
-    rc = hip_check(hipMemcpy(&w, ws, sizeof(w), hipMemcpyDeviceToHost), who);
+    int rc = hip_check(hipMemcpyAsync(&w, ws, sizeof(w), hipMemcpyDeviceToHost, s), who);
+    if (rc == RDN_OK) rc = hip_check(hipStreamSynchronize(s), who);
     if (rc != RDN_OK) return rc;
     if (!w) return RDN_OK;
     if (flags) *flags = w & (RDN_STATUS_RANGE | RDN_STATUS_GATE);

@@ -1796,19 +1796,21 @@ hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes
   *timed_out = 0;
   *out_of_range = 0;
   *gate = 0;
-  hipError_t e = hipStreamSynchronize(stream);
-  if (e != hipSuccess) return e;
+  hipError_t e = hipSuccess;
   const TeamGeo tg = team_geo(arch, team_mode(dtype), L, stream_device(stream));
   unsigned* words;
   if (tg.teams <= 0) {
-    if (!ws) return hipSuccess;
+    if (!ws) return hipStreamSynchronize(stream);
     words = seg_range(ws);                                              // [1] range, [2] gate (sticky)
   } else {
     if (!ws || ws_bytes < tg.total) return hipErrorInvalidValue;
     words = team_err(tg, ws);                                           // [1] timeout, [2] range, [3] gate
   }
+  // the words' copy is ordered behind the forwards on their stream; one wait covers both (the
+  // batch-1 module path pays this per call)
   unsigned w[4] = {0, 0, 0, 0};
-  e = hipMemcpy(w, words, sizeof(w), hipMemcpyDeviceToHost);
+  e = hipMemcpyAsync(w, words, sizeof(w), hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
   if (e != hipSuccess) return e;
   if (tg.teams <= 0) {
     *out_of_range = w[1] != 0;
