@@ -50,6 +50,9 @@ template <int NBK> struct TileGeo {
 #ifndef RDN_HALF_REMAP
 #define RDN_HALF_REMAP 0
 #endif
+#ifndef RDN_TAIL_STAG
+#define RDN_TAIL_STAG 0       // diagnostic A/B: the in-place write-back of waves 4-7 one k-step late
+#endif
 template <int NBK> struct WalkGeo {
   static constexpr int WB = RDN_WALK_ROWS_MIX;
   static constexpr bool HALF = WB == 128 * NBK - 64;
@@ -748,6 +751,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   constexpr bool REMAP = TG::HALF && RDN_HALF_REMAP;
   static_assert(!REMAP || MODE == MODE_H8, "the half-block remap is written for the f16 + e4m3 write-back");
   const bool half_idle = TG::HALF && !REMAP && (__builtin_amdgcn_readfirstlane(tid >> 6) >> 1) >= 2;
+  const bool stag_late = RDN_TAIL_STAG && __builtin_amdgcn_readfirstlane(tid >> 6) >= 4;
   const uint32_t hoff = REMAP ? (uint32_t)(16 * ROWB_F32) * (uint32_t)__builtin_amdgcn_readfirstlane(nq) : 0u;
   // the remapped block's rows of this wave start 16 nq, not 32 nq, rows into it
   auto remapped = [&](int j) { return REMAP && j == NB - 1; };
@@ -999,7 +1003,15 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
       }
       if (j >= 2 && !beyond(j - 2)) {
         constexpr int NP = NT * MT;
-        if constexpr (MODE == MODE_H8) {
+        if constexpr (MODE == MODE_H8 && RDN_TAIL_STAG) {
+          // waves 4-7 (row quarters 2-3) share their SIMDs with waves 0-3: their write-backs run one
+          // k-step later, so the two waves of a SIMD do not issue their e4m3-split VALU together
+          if (!stag_late) {
+            if (s < NT) store_pair(j - 2, s);
+          } else if (s >= 1 && s - 1 < NT) {
+            store_pair(j - 2, s - 1);
+          }
+        } else if constexpr (MODE == MODE_H8) {
           if (s < NT) store_pair(j - 2, s);
         } else if constexpr (O::KSTEPS >= NP) {
           if (s < NP) store_piece(j - 2, s / MT, s % MT);
