@@ -17,7 +17,7 @@ namespace met {
 template <typename TC>
 __global__ __launch_bounds__(MET_THREADS) void metrics_kernel(const float* __restrict__ y, const TC* __restrict__ clean,
                                                               int L, MetricOut mo) {
-  __shared__ double red[MET_THREADS / 64];
+  __shared__ double red[RED_DOUBLES];
   const int64_t n = __builtin_amdgcn_workgroup_id_x();
   const float* yy = y + (size_t)n * L;
   spectrum_metrics([&](int p) { return yy[p]; }, clean + (size_t)n * L, L, n, red, mo);

@@ -32,6 +32,28 @@ __device__ __forceinline__ T block_reduce(T v, T* scratch, Op op) {
   for (int i = 1; i < MET_THREADS / 64; ++i) r = op(r, scratch[i]);
   return r;
 }
+// Six reductions in one round trip through the scratch (each value reduced exactly as block_reduce
+// would: lane butterfly, then the waves in order): sums [0, 2), maxima [2, 4), minima [4, 6)
+constexpr int RED_DOUBLES = 6 * (MET_THREADS / 64);
+__device__ __forceinline__ void block_reduce6(double (&v)[6], double* scratch) {
+  const int w = __builtin_amdgcn_workitem_id_x() >> 6, lane = __builtin_amdgcn_workitem_id_x() & 63;
+  auto op = [](int k, double a, double b) { return k < 2 ? a + b : k < 4 ? (a > b ? a : b) : (a < b ? a : b); };
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+    for (int o = 32; o > 0; o >>= 1) v[k] = op(k, v[k], __shfl_xor(v[k], o));
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) scratch[k * (MET_THREADS / 64) + w] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    double r = scratch[k * (MET_THREADS / 64)];
+    for (int i = 1; i < MET_THREADS / 64; ++i) r = op(k, r, scratch[k * (MET_THREADS / 64) + i]);
+    v[k] = r;
+  }
+}
 
 // Limb j (32 bits at weight 2^(32 j - RDN_ACC_FRAC_BITS)) of the fixed-point image of v, truncated
 // toward zero below 2^-128, signed like v.  Returns false if |v| >= 2^64 or v is not finite (the
@@ -58,15 +80,13 @@ __device__ __forceinline__ bool to_limbs(double v, long long (&limb)[RDN_ACC_LIM
 }
 
 // The four metrics of spectrum n (denoised values through yv(p), clean cc[0..L)), every thread of the
-// MET_THREADS-thread workgroup taking part; red: MET_THREADS / 64 doubles of LDS.  Results: per[n],
+// MET_THREADS-thread workgroup taking part; red: RED_DOUBLES doubles of LDS.  Results: per[n],
 // sums, acc of mo (each optional).
 template <typename TC, class YV>
 __device__ __forceinline__ void spectrum_metrics(YV yv, const TC* __restrict__ cc, int L, int64_t n, double* red,
                                                  const MetricOut& mo) {
   const int tid = __builtin_amdgcn_workitem_id_x();
   const auto add = [](double a, double b) { return a + b; };
-  const auto mx = [](double a, double b) { return a > b ? a : b; };
-  const auto mn = [](double a, double b) { return a < b ? a : b; };
 
   double se = 0.0, sm = 0.0, ymax = -INFINITY, ymin = INFINITY, cmax = -INFINITY, cmin = INFINITY;
   for (int p = tid; p < L; p += MET_THREADS) {
@@ -78,12 +98,9 @@ __device__ __forceinline__ void spectrum_metrics(YV yv, const TC* __restrict__ c
     cmax = fmax(cmax, c);
     cmin = fmin(cmin, c);
   }
-  se = block_reduce(se, red, add);
-  sm = block_reduce(sm, red, add);
-  ymax = block_reduce(ymax, red, mx);
-  ymin = block_reduce(ymin, red, mn);
-  cmax = block_reduce(cmax, red, mx);
-  cmin = block_reduce(cmin, red, mn);
+  double r6[6] = {se, sm, ymax, cmax, ymin, cmin};
+  block_reduce6(r6, red);
+  se = r6[0], sm = r6[1], ymax = r6[2], cmax = r6[3], ymin = r6[4], cmin = r6[5];
 
   const double R = cmax - cmin;
   const double C1 = (0.01 * R) * (0.01 * R), C2 = (0.03 * R) * (0.03 * R);
@@ -100,8 +117,10 @@ __device__ __forceinline__ void spectrum_metrics(YV yv, const TC* __restrict__ c
       syy += b * b;
       sxy += a * b;
     }
-    const double ux = sx / 7, uy = sy / 7;
-    const double vx = cov * (sxx / 7 - ux * ux), vy = cov * (syy / 7 - uy * uy), vxy = cov * (sxy / 7 - ux * uy);
+    // window means by one multiplication each (five fp64 divisions per window were most of the loop)
+    constexpr double inv7 = 1.0 / 7.0;
+    const double ux = sx * inv7, uy = sy * inv7;
+    const double vx = cov * (sxx * inv7 - ux * ux), vy = cov * (syy * inv7 - uy * uy), vxy = cov * (sxy * inv7 - ux * uy);
     ss += ((2 * ux * uy + C1) * (2 * vxy + C2)) / ((ux * ux + uy * uy + C1) * (vx + vy + C2));
   }
   ss = block_reduce(ss, red, add);
@@ -163,7 +182,7 @@ __device__ __forceinline__ void walk_metrics_t(const float* y, const TC* cc, int
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)y, 0, L * 4, 0x00020000);
   const auto yg = [&](int p) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yr, 4 * p, 0, 16)); };
   double* red = (double*)lds;
-  constexpr int RED = 64, LDS_MAX = 163840;
+  constexpr int RED = RED_DOUBLES * 8, LDS_MAX = 163840;
   const int yb = (L * 4 + 15) & ~15;
   if (RED + yb + (size_t)L * sizeof(TC) <= (size_t)LDS_MAX) {
     float* ys = (float*)(lds + RED);
