@@ -19,10 +19,10 @@ import shutil
 import sys
 
 # round 5: batch 8192 runs the walk kernels (abi.cpp walk_tiles)
-KERNELS = {"f16": "rdn::ip::rrcdnet_hybrid_walk<5>", "f16-plain": "rdn::h16fw::rrcdnet_walk", "f16f8": "rdn::ip::rrcdnet<3, 0>",
+KERNELS = {"f16": "rdn::ip::rrcdnet_hybrid_walk<5, false>", "f16-plain": "rdn::h16fw::rrcdnet_walk", "f16f8": "rdn::ip::rrcdnet<3, 0>",
            "bf16x3": "rdn::ip::rrcdnet<2, 0>", "bf16-unsafe": "rdn::h16::rrcdnet"}
 # scripts/gpu_final.sh passes: pmc_<arch>-<dtype>_<counter>, batch per arch
-KERNELS_FINAL = {("RRCDNet", "f16"): ("rdn::ip::rrcdnet_hybrid_walk<5>", 8192),
+KERNELS_FINAL = {("RRCDNet", "f16"): ("rdn::ip::rrcdnet_hybrid_walk<5, false>", 8192),
                  ("RRCDNet", "f16-plain"): ("rdn::h16fw::rrcdnet_walk", 8192),
                  ("ADSDN", "f16"): ("rdn::cb::team16_forward<true>", 2048),
                  ("APIDN", "f16"): ("rdn::cb::team16_forward<false>", 2048)}
