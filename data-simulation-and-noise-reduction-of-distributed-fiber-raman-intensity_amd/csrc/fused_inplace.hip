@@ -3,6 +3,8 @@
 //
 // Reference forwards: 1DCNN/train.py:71-82, RRCDNet/train.py:72-98, DSDN/train.py:72-126,
 // PIDN/train.py:72-106.
+#include <cstddef>
+
 #include "inplace.hpp"
 #include "host_util.hpp"
 #include "metrics.hpp"
@@ -379,6 +381,8 @@ struct HybWalkArgs {
   unsigned* status;
   met::MetricOut mo;
 };
+static_assert(offsetof(HybWalkArgs, y) == 16 && offsetof(HybWalkArgs, L) == 24 && offsetof(HybWalkArgs, mo) == 48,
+              "HybWalkArgs mirrors rrcdnet_hybrid_walk's parameters (kernarg layout: natural alignment, in order)");
 template <int TAIL, bool MET>
 __global__ __launch_bounds__(THREADS) void rrcdnet_hybrid_walk(const uint8_t* __restrict__ blob,
                                                                const float* __restrict__ x, float* __restrict__ y,

@@ -182,7 +182,7 @@ class _EngineNet(nn.Module):
         ws = self._workspace(x)
         range_why = "activations beyond the e4m3 planes' range (|v| > 1792)"
         gate_why = f"|input| beyond {INPUT_GATE} (outside normalised intensity)"
-        cbam = engine.ARCH_ID[self.ARCH] in engine.CBAM_IDS
+        cbam = self.ARCH in engine.CBAM_ARCHS
         flags = 0
         try:
             # a fused network's status word is read below (the call's one 4-byte host read); a CBAM
