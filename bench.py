@@ -68,7 +68,10 @@ def flops_per_spectrum(arch, L):
     return per_pos * L
 
 
-def index_blocks(world, rank, B, steps_pipeline=3, B4=8192, chunks4=4):
+PIPELINE_STEPS = 8          # timed steps per pipeline leg (each leg ~0.5 s at the default batch)
+
+
+def index_blocks(world, rank, B, steps_pipeline=PIPELINE_STEPS, B4=8192, chunks4=4):
     """Simulator spectrum indices each leg of rank `rank` generates (half-open ranges): the headline
     batch, the pipeline's steps + 1 batches, and the config-4 driver's total (evaluate_synthetic
     shards [first, first + total) over the ranks itself).  Disjoint across legs and ranks."""
@@ -564,7 +567,7 @@ def main():
     torch.manual_seed(1234)                       # random-init weights of the architecture
     model = R.MODELS[args.arch]().to(dev).eval().set_engine_dtype(args.dtype)
     B, L = args.batch, args.L
-    blocks = index_blocks(world, rank, B, 3, args.config4_batch, args.config4_chunks)
+    blocks = index_blocks(world, rank, B, PIPELINE_STEPS, args.config4_batch, args.config4_chunks)
     clean, noisy, _, _ = engine.generate(B, args.seed, first_index=blocks["headline"][0], signal_length=L, device=dev)
     x = noisy.view(B, 1, L)
     y = torch.empty_like(x)
@@ -639,9 +642,9 @@ def main():
     pipeline = None
     if not args.no_pipeline:
         progress("pipeline")
-        # each rank's pipeline block of 4*B indices after every rank's headline batch (index_blocks)
+        # each rank's pipeline block of (PIPELINE_STEPS + 1)*B indices after every rank's headline batch
         pipeline = time_pipeline(engine, args.arch, code, packed, args.seed, blocks["pipeline"][0], B, L,
-                                 3, stream, dev)
+                                 PIPELINE_STEPS, stream, dev)
 
     sustained = None
     if args.sustained_seconds > 0:

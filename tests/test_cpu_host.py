@@ -223,13 +223,13 @@ def test_bench_index_blocks_disjoint(world):
     B, B4, chunks = 8192, 8192, 4
     ranges = []
     for r in range(world):
-        b = bench.index_blocks(world, r, B, 3, B4, chunks)
+        b = bench.index_blocks(world, r, B, bench.PIPELINE_STEPS, B4, chunks)
         ranges += [b["headline"], b["pipeline"]]
         lo, hi = shard(b["config4_total"], r, world)
         ranges.append((b["config4_first"] + lo, b["config4_first"] + hi))
     ranges.append((b["config4_warmup_first"], b["config4_warmup_first"] + 2 * world))
     for r in range(world):                  # the sustained window: up to 2^32 indices per rank
-        s0 = bench.index_blocks(world, r, B, 3, B4, chunks)["sustained_first"]
+        s0 = bench.index_blocks(world, r, B, bench.PIPELINE_STEPS, B4, chunks)["sustained_first"]
         ranges.append((s0, s0 + (1 << 32)))
     ranges.sort()
     assert all(a[1] <= c[0] for a, c in zip(ranges, ranges[1:])), ranges
