@@ -123,14 +123,15 @@ def evaluate(model, noisy_data, clean_data, batch_size=1024, device=None):
 
 
 def evaluate_synthetic(models, total, seed=20250410, signal_length=10000, batch_size=8192, device=None,
-                       first_index=0, gen_kwargs=None, log_every_s=0.0):
+                       first_index=0, gen_kwargs=None, log_every_s=0.0, fused_metrics=True):
     """Config 4: ``total`` simulator spectra [first_index, first_index + total),
     sharded over the ranks as [r·N/W, (r+1)·N/W), each chunk generated on the device, denoised by
     every model in ``models`` (name -> module) and metered into that model's exact accumulator.
     Returns {name: {"means", "spectra", "seconds", "spectra_per_s"}} with the all-reduced means
     (identical for any world size) and the max-over-ranks wall time of the loop.  ``log_every_s`` > 0
     prints progress to stderr about that often (the loop then waits for the device every 64 chunks,
-    so the printed count is what the GPU has finished)."""
+    so the printed count is what the GPU has finished).  ``fused_metrics=False`` meters with the separate
+    metrics kernel after each forward (the A/B of the metric epilogue; the same bits)."""
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device())
     device = torch.device(device)
@@ -166,8 +167,13 @@ def evaluate_synthetic(models, total, seed=20250410, signal_length=10000, batch_
                                 out=(clean[:nb], noisy[:nb]), **gen_kwargs)
                 # forward + metric sums in one call: on the walk geometry the forward kernel meters each
                 # spectrum itself (no second pass over y); otherwise the metrics kernel follows it
-                engine.forward_metrics(model.ARCH, model.engine_code, packed, noisy[:nb].view(nb, 1, L), clean[:nb],
-                                       out=y[:nb], acc=acc, check=False, workspace=ws)
+                if fused_metrics:
+                    engine.forward_metrics(model.ARCH, model.engine_code, packed, noisy[:nb].view(nb, 1, L),
+                                           clean[:nb], out=y[:nb], acc=acc, check=False, workspace=ws)
+                else:
+                    engine.forward(model.ARCH, model.engine_code, packed, noisy[:nb].view(nb, 1, L), out=y[:nb],
+                                   check=False, workspace=ws)
+                    engine.metrics(y[:nb].view(nb, L), clean[:nb], per_spectrum=False, acc=acc)
             _finish(model, ws)              # waits for the stream; raises on a timed-out hand-off / range / gate
             torch.cuda.synchronize(device)
             el = time.perf_counter() - t0

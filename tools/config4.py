@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--weights", default="trained", choices=["trained", "random"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--out", default=None)
+    ap.add_argument("--no-fused-metrics", action="store_true",
+                    help="meter with the separate metrics kernel (A/B of rdn_forward_metrics' epilogue)")
     args = ap.parse_args()
 
     distributed = "WORLD_SIZE" in os.environ
@@ -65,11 +67,11 @@ def main():
         models[a] = m.to(dev).eval().set_engine_dtype(args.dtype)
     evaluate_synthetic(models, 2 * W, seed=args.seed, signal_length=args.L, batch_size=2, device=dev)   # warm-up
     res = evaluate_synthetic(models, args.total, seed=args.seed, signal_length=args.L, batch_size=args.batch,
-                             device=dev, log_every_s=30.0)
+                             device=dev, log_every_s=30.0, fused_metrics=not args.no_fused_metrics)
     if rank == 0:
         rec = {"config": "BASELINE.json configs[3]", "total_spectra": args.total, "n_gpus": W,
                "dist_backend": args.dist_backend if distributed else None, "dtype": args.dtype, "L": args.L,
-               "batch_per_rank": args.batch, "weights": args.weights,
+               "batch_per_rank": args.batch, "weights": args.weights, "fused_metrics": not args.no_fused_metrics,
                "networks": {a: {k: v for k, v in r.items()} for a, r in res.items()}}
         line = json.dumps(rec)
         print(line, flush=True)
