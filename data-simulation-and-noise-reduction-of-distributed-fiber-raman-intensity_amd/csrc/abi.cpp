@@ -327,8 +327,7 @@ static int forward_status(const char* who, int arch, int dtype, int64_t n, int64
     if (!status_word(dtype) || !ws || ws_bytes < RANGE_WS_BYTES) return hip_check(hipStreamSynchronize(s), who);
     // the word's copy is ordered behind the forwards on their stream: one wait covers both
     unsigned w = 0;
-    int rc = hip_check(hipMemcpyAsync(&w, ws, sizeof(w), hipMemcpyDeviceToHost, s), who);
-    if (rc == RDN_OK) rc = hip_check(hipStreamSynchronize(s), who);
+    int rc = hip_check(rdn::read_words(&w, ws, sizeof(w), s), who);
     if (rc != RDN_OK) return rc;
     if (!w) return RDN_OK;
     if (flags) *flags = w & (RDN_STATUS_RANGE | RDN_STATUS_GATE);

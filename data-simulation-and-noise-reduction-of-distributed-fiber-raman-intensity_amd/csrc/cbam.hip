@@ -1566,8 +1566,7 @@ static int team_lds(int mode) { return mode == MODE_P16 ? (int)h16c::LDS_BYTES :
 // the team kernel RDN_<dtype> runs (RDN_F16: the ping-pong one)
 static int team_mode(int dtype) { return dtype == F16 ? MODE_P16 : dtype_mode(dtype); }
 
-// co-resident workgroups per CU of the team kernel on `dev` (0 on any failure)
-static int team_blocks_per_cu(int arch, int mode, int dev) {
+static int team_blocks_query(int arch, int mode, int dev) {
   const void* k = team_fn(arch, mode);
   if (ensure_dynamic_lds(k, team_slot(arch, mode), team_lds(mode), dev) != hipSuccess) {
     (void)hipGetLastError();          // no team geometry (the segment path runs); leave no sticky error behind
@@ -1578,6 +1577,20 @@ static int team_blocks_per_cu(int arch, int mode, int dev) {
   if (cur != dev && hipSetDevice(dev) != hipSuccess) return 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, THREADS, team_lds(mode)) != hipSuccess) nb = 0;
   if (cur != dev) (void)hipSetDevice(cur);
+  return nb;
+}
+
+// co-resident workgroups per CU of the team kernel on `dev` (0 on any failure), cached per (kernel,
+// device): the occupancy query ran three times per call of the batch-1 loop (the forward's workspace
+// check and launch, the status read)
+static int team_blocks_per_cu(int arch, int mode, int dev) {
+  static std::atomic<int> known[MAX_DEVICES * ATTR_SLOTS];           // blocks + 1; 0 = not queried yet
+  const int slot = team_slot(arch, mode);
+  if (dev < 0 || dev >= MAX_DEVICES) return 0;
+  const int c = known[dev * ATTR_SLOTS + slot].load(std::memory_order_relaxed);
+  if (c > 0) return c - 1;
+  const int nb = team_blocks_query(arch, mode, dev);
+  known[dev * ATTR_SLOTS + slot].store(nb + 1, std::memory_order_relaxed);
   return nb;
 }
 
@@ -1809,8 +1822,7 @@ hipError_t cbam_status(int arch, int dtype, int64_t L, void* ws, size_t ws_bytes
   // the words' copy is ordered behind the forwards on their stream; one wait covers both (the
   // batch-1 module path pays this per call)
   unsigned w[4] = {0, 0, 0, 0};
-  e = hipMemcpyAsync(w, words, sizeof(w), hipMemcpyDeviceToHost, stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  e = read_words(w, words, sizeof(w), stream);
   if (e != hipSuccess) return e;
   if (tg.teams <= 0) {
     *out_of_range = w[1] != 0;

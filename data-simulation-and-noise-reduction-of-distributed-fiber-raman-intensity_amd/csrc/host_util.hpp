@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstring>
 #include <mutex>
 
 namespace rdn {
@@ -54,6 +55,29 @@ inline hipError_t ensure_dynamic_lds(const void* fn, int slot, int bytes, int de
     if (e == hipSuccess) e = e2;
   }
   if (e == hipSuccess) flag.store(true, std::memory_order_release);
+  return e;
+}
+
+// Copy `bytes` (<= 16) of status words from the device to `out` behind the work on `s` and wait for
+// it: through a 16-byte pinned buffer of the calling thread (a copy into pageable memory takes the
+// runtime's staging path, ≈ 20 µs more per call of the batch-1 loop).  The buffer is allocated on
+// the thread's first read and kept (16 B per thread that ever read a status word); stack memory if
+// the allocation fails.
+inline hipError_t read_words(void* out, const void* dev_words, size_t bytes, hipStream_t s) {
+  thread_local void* pinned = nullptr;
+  thread_local bool tried = false;
+  if (!tried) {
+    tried = true;
+    if (hipHostMalloc(&pinned, 16, hipHostMallocPortable) != hipSuccess) {
+      pinned = nullptr;
+      (void)hipGetLastError();
+    }
+  }
+  if (bytes > 16) return hipErrorInvalidValue;
+  void* dst = pinned ? pinned : out;
+  hipError_t e = hipMemcpyAsync(dst, dev_words, bytes, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess && pinned) memcpy(out, pinned, bytes);
   return e;
 }
 

@@ -182,12 +182,11 @@ class _EngineNet(nn.Module):
         ws = self._workspace(x)
         range_why = "activations beyond the e4m3 planes' range (|v| > 1792)"
         gate_why = f"|input| beyond {INPUT_GATE} (outside normalised intensity)"
-        cbam = self.ARCH in engine.CBAM_ARCHS
         flags = 0
         try:
-            # a fused network's status word is read below (the call's one 4-byte host read); a CBAM
-            # network's status words are read and cleared by one rdn_forward_status_ex call (its input
-            # gate included: no aminmax pass, no second sync).  With a blob packed earlier for
+            # the status words (a fused network's one word, a CBAM network's four) are read and cleared
+            # by one rdn_forward_status_ex call (the input gate included: no aminmax pass, no second
+            # sync).  With a blob packed earlier for
             # this device and dtype, a fused network launches first and checks the pack cache after
             # (a key over every parameter and buffer: ~15 us of host time, evaulate.py's batch-1 loop
             # calls this per spectrum), so the check runs while the kernel does; weights changed since
@@ -200,21 +199,16 @@ class _EngineNet(nn.Module):
             if spec and self._state_key(dev) != self._packed_key:
                 y = engine.forward(self.ARCH, code, self.packed_weights(dev), x, out=y, check=False, workspace=ws,
                                    _ws_checked=True)
-            if cbam:
-                flags = ws.check()            # waits; raises on a timed-out hand-off (EngineError) or RangeError
+            if ws is not None:
+                # waits; raises on a timed-out hand-off (EngineError) or RangeError.  The kernels' stems
+                # raise the input-gate bit (they read every x), the corrected layers the range bit: no
+                # extra kernel, one wait, one 4-16 byte copy into a pinned buffer (abi.cpp read_words)
+                flags = ws.check()
         except _lib.RangeError:
             # an activation left the e4m3 planes' range: never return the NaN tiles
             why = range_why
-        if why is None and code != 0 and x.numel():
-            if not cbam and ws is not None:
-                # the kernels' stems raise the input-gate bit (they read every x), the corrected
-                # layers the range bit: no extra kernel, one wait
-                w = int(ws.status_word().item())
-                if w:
-                    ws.clear_status_word()
-                    why = range_why if w & engine.STATUS_RANGE else gate_why
-            elif flags & engine.STATUS_GATE:                  # CBAM networks: the stems raised the gate
-                why = gate_why
+        if why is None and code != 0 and x.numel() and flags & engine.STATUS_GATE:
+            why = gate_why
         if why is None:
             return y
         # the batch is re-run in exact fp32, which has neither bound
