@@ -50,6 +50,11 @@ template <int NBK> struct TileGeo {
 #ifndef RDN_HALF_REMAP
 #define RDN_HALF_REMAP 0
 #endif
+#ifndef RDN_TAIL_SGB
+// A/B: the corrected layers' write-back VALU (e4m3 split of block j-2) interleaved between the last
+// N-tile's MFMAs of the k-step, RDN_TAIL_SGB VALU per MFMA (sched_group_barrier); 0 = off
+#define RDN_TAIL_SGB 0
+#endif
 #ifndef RDN_TAIL_STAG
 #define RDN_TAIL_STAG 0       // diagnostic A/B: the in-place write-back of waves 4-7 one k-step late
 #endif
@@ -752,6 +757,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   static_assert(!REMAP || MODE == MODE_H8, "the half-block remap is written for the f16 + e4m3 write-back");
   const bool half_idle = TG::HALF && !REMAP && (__builtin_amdgcn_readfirstlane(tid >> 6) >> 1) >= 2;
   const bool stag_late = RDN_TAIL_STAG && __builtin_amdgcn_readfirstlane(tid >> 6) >= 4;
+  constexpr bool SGB = RDN_TAIL_SGB && !RDN_TAIL_STAG && MODE == MODE_H8 && cin && !(EPI & (ADD_ID | SAVE_ID));
   const uint32_t hoff = REMAP ? (uint32_t)(16 * ROWB_F32) * (uint32_t)__builtin_amdgcn_readfirstlane(nq) : 0u;
   // the remapped block's rows of this wave start 16 nq, not 32 nq, rows into it
   auto remapped = [&](int j) { return REMAP && j == NB - 1; };
@@ -967,6 +973,24 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
         if (s + 1 < O::KSTEPS) bnext[i] = read_b(j, s + 1, i);
         else if (j + 1 < NB && !(j + 1 == NB - 1 && half_idle) && !(remapped(j + 1) && i > 0)) bnext[i] = read_b(j + 1, 0, i);
         }
+        if constexpr (SGB) {
+          if (i == NT - 1 && j >= 2 && s < NT && !beyond(j - 2)) {
+            store_pair(j - 2, s);
+            // MFMA, B read, V VALU (x4), MFMA, V VALU (x2), the three plane stores
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, RDN_TAIL_SGB, 0);
+            }
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, RDN_TAIL_SGB, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
+          }
+        }
         if constexpr (COMP) {
           // fold a finished chunk into the running totals (the rounding error becomes the next
           // chunk's accumulator start), staggered by one N-tile so that the VALU neither waits for
@@ -1012,7 +1036,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
             store_pair(j - 2, s - 1);
           }
         } else if constexpr (MODE == MODE_H8) {
-          if (s < NT) store_pair(j - 2, s);
+          if (!SGB && s < NT) store_pair(j - 2, s);
         } else if constexpr (O::KSTEPS >= NP) {
           if (s < NP) store_piece(j - 2, s / MT, s % MT);
         } else {

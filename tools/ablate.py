@@ -25,7 +25,8 @@ VARIANTS = {"base": "", "prev": "", "cur": "", "cur2": "", "nolds": "-DRDN_ABLAT
             "w512": "-DRDN_WALK_ROWS=512", "w448": "-DRDN_WALK_ROWS=448", "mix512": "-DRDN_WALK_ROWS_MIX=512", "mhead": "", "lbar": "", "stg": "", "vote": "", "comb": "", "track": "", "trk2": "", "sdpp": "", "cur": "", "resplain": "", "rescomp0": "-DRDN_F32_COMP_RES=0", "reschunk6": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=6", "reschunk3": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=3", "reschunk4": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=4", "reschunk2": "-DRDN_F32_COMP_RES=1 -DRDN_F32_CHUNK_RES=2", "nozero": "-DRDN_ABLATE_NOZERO", "nozst": "-DRDN_ABLATE_NOZERO -DRDN_TEAM_STAMPS=1", "estag": "-DRDN_H16_ESTAG=1",
             "prio": "-DRDN_SETPRIO=1", "prio2": "-DRDN_SETPRIO=2", "es3": "-DRDN_H16_ESPLIT=3", "es5": "-DRDN_H16_ESPLIT=5",
             "sgb2": "-DRDN_H16_SGB=2", "sgb4": "-DRDN_H16_SGB=4", "remap": "-DRDN_HALF_REMAP=1",
-            "prioremap": "-DRDN_SETPRIO=1 -DRDN_HALF_REMAP=1", "tstag": "-DRDN_TAIL_STAG=1"}
+            "prioremap": "-DRDN_SETPRIO=1 -DRDN_HALF_REMAP=1", "tstag": "-DRDN_TAIL_STAG=1",
+            "tsgb1": "-DRDN_TAIL_SGB=1", "tsgb2": "-DRDN_TAIL_SGB=2", "tsgb4": "-DRDN_TAIL_SGB=4", "tsgb8": "-DRDN_TAIL_SGB=8"}
 
 
 def build():
