@@ -50,6 +50,12 @@ template <int NBK> struct TileGeo {
 #ifndef RDN_HALF_REMAP
 #define RDN_HALF_REMAP 0
 #endif
+#ifndef RDN_TAIL_EARLY
+#define RDN_TAIL_EARLY 0      // A/B: next-layer operand loads of the half block's idle waves one block early
+#endif
+#ifndef RDN_STAGE_FIRST
+#define RDN_STAGE_FIRST 0     // A/B (the hybrid walk): layer 9's plane stores before the tail's operand loads
+#endif
 #ifndef RDN_TAIL_SGB
 // A/B: the corrected layers' write-back VALU (e4m3 split of block j-2) interleaved between the last
 // N-tile's MFMAs of the k-step, RDN_TAIL_SGB VALU per MFMA (sched_group_barrier); 0 = off
@@ -651,10 +657,19 @@ __device__ __forceinline__ uint32_t load_scale(const uint8_t* wl, int m) {
   return MODE == MODE_H8 ? ((const uint32_t*)(wl + H8_SCALE_OFF))[m * 64 + (__builtin_amdgcn_workitem_id_x() & 63)] : 0u;
 }
 
-template <int MODE>
+template <int MODE, bool SOUTER = false>
 __device__ __forceinline__ void load_layer_a(const Tile& tl, int layer, LayerA<MODE>& a) {
   const int tid = opaque_tid(), mp = (tid >> 6) & 1, lane = tid & 63;
   const uint8_t* wl = tl.big + (size_t)layer * LayerBytes<MODE>::BYTES;
+  if constexpr (SOUTER) {            // k-step outer: the first k-step's fragments of both M-tiles first
+#pragma unroll
+    for (int mm = 0; mm < IP_MT; ++mm) a.bias[mm] = load_bias<MODE>(wl, IP_MT * mp + mm), a.sc[mm] = load_scale<MODE>(wl, IP_MT * mp + mm);
+#pragma unroll
+    for (int s = 0; s < Op<MODE>::KSTEPS; ++s)
+#pragma unroll
+      for (int mm = 0; mm < IP_MT; ++mm) a[mm][s] = Op<MODE>::load_a(wl, IP_MT * mp + mm, s, lane);
+    return;
+  }
 #pragma unroll
   for (int mm = 0; mm < IP_MT; ++mm) {
     a.bias[mm] = load_bias<MODE>(wl, IP_MT * mp + mm);
@@ -830,6 +845,21 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
     }
 
   f32x4 res[NB][NT][MT];
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+  // diagnostic (tools/hyb_stamps.py, walk): wave 0's time per block of each corrected walk layer, from
+  // the layer's start (block 0 includes the operand wait) to each block's barrier, then the last two
+  // write-backs; summed into the status workspace's words 16 + j (one atomic per block and layer)
+  unsigned long long bst_t = __builtin_amdgcn_s_memtime(), bst[NB + 1];
+#pragma unroll
+  for (int k = 0; k <= NB; ++k) bst[k] = 0;
+  auto bstamp = [&](int k) {
+    const unsigned long long nt = __builtin_amdgcn_s_memtime();
+    bst[k] += nt - bst_t;
+    bst_t = nt;
+  };
+#else
+  auto bstamp = [&](int) {};
+#endif
   // write-back of N-tile i, M-tile mm of block j (bias / identity, ReLU, zero padding, round)
   auto store_piece = [&](int j, int i, int mm) {
     const int rb = BR * j + (BR / 4) * nq;            // first row of this wave's share of block j
@@ -897,6 +927,14 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   // positions), so the block skips its MFMAs, B reads and write-back (its rows keep older values,
   // which only feed rows beyond L: never stored, never tracked by the range guard)
   auto beyond = [&](int j) { return WALK && EDGE && tl.base + BR * j >= tl.L + 8; };
+  // the block whose k-steps retire this layer's operands, after which the next layer's are fetched: the
+  // last block; RDN_TAIL_EARLY: for the waves that own no rows of a last half block, the block before
+  // (their last use), so half of the CU's operand loads -- bound by the texture path, ~3k cycles per
+  // corrected layer -- leave a block earlier instead of queueing with the others' in the half block
+  auto load_next = [&](int j) {
+    if constexpr (RDN_TAIL_EARLY && TG::HALF && !REMAP) return half_idle ? j == NB - 2 : j == NB - 1;
+    return j == NB - 1;
+  };
   auto store_block = [&](int j) {
     if ((j == NB - 1 && half_idle) || beyond(j)) return;
     if constexpr (MODE == MODE_H8) {
@@ -935,7 +973,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #pragma unroll
         for (int mm = 0; mm < MT; ++mm) hi[i][mm] = bias_l[mm];
     }
-    if (j == NB - 1 && has_next) {                    // last use of this layer's bias
+    if (has_next && load_next(j)) {                   // last use of this layer's bias
 #pragma unroll
       for (int mm = 0; mm < MT; ++mm) a.bias[mm] = load_bias<MODE>(wnext, MT * mp + mm), a.sc[mm] = load_scale<MODE>(wnext, MT * mp + mm);
     }
@@ -1010,7 +1048,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (j == NB - 1 && has_next) {                                   // last use of a[.][s]
+      if (has_next && load_next(j)) {                                  // last use of a[.][s]
 #pragma unroll
         for (int mm = 0; mm < MT; ++mm) {
           if constexpr (MODE == MODE_H8 && !LOADC) O::load_a_main(wnext, MT * mp + mm, s, lane, a[mm][s]);
@@ -1064,10 +1102,18 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #else
     lds_barrier();                 // every wave is done reading the rows block j needed
 #endif
+    bstamp(j);
   }
   store_block(NB - 2);
   store_block(NB - 1);
   lds_barrier();                   // the layer's output is complete
+  bstamp(NB);
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+  if (WALK && MODE == MODE_H8 && tl.status && tid == 0) {
+#pragma unroll
+    for (int k = 0; k <= NB; ++k) atomicAdd((unsigned long long*)tl.status + 16 + k, bst[k]);
+  }
+#endif
   tl.layer += 1;
   if constexpr (WALK) {
     tl.cs_prev = tl.cs_cur;

@@ -105,9 +105,17 @@ __device__ __forceinline__ void tile(Tile& tl, PP::Tile& t16, float* y, int t, i
   {
     H8Stage stg;
     PP::layer<PP::STAGE, EDGE>(t16, PP::BUF1, PP::BUF0, 1, F1, F0, false, nullptr, nullptr, &stg);
+#if RDN_STAGE_FIRST
+    // A/B: the planes' LDS stores ahead of the tail's 26 operand loads per wave (whose issue waits on
+    // the texture path), the loads k-step-outer so the first k-step's fragments arrive first
+    stg.write<EDGE>(tl.lds, t16);
+    stage_carry(tl.lds, t16);
+    load_layer_a<MODE_H8, true>(tl, PPL + 1, a);
+#else
     load_layer_a<MODE_H8>(tl, PPL + 1, a);
     stg.write<EDGE>(tl.lds, t16);
     stage_carry(tl.lds, t16);
+#endif
     tl.amax = fmaxf(tl.amax, stg.amax);
   }
   // hand the walk state to the in-place tile: its logical row 0 is buffer row CG

@@ -26,7 +26,9 @@ VARIANTS = {"base": "", "prev": "", "cur": "", "cur2": "", "nolds": "-DRDN_ABLAT
             "prio": "-DRDN_SETPRIO=1", "prio2": "-DRDN_SETPRIO=2", "es3": "-DRDN_H16_ESPLIT=3", "es5": "-DRDN_H16_ESPLIT=5",
             "sgb2": "-DRDN_H16_SGB=2", "sgb4": "-DRDN_H16_SGB=4", "remap": "-DRDN_HALF_REMAP=1",
             "prioremap": "-DRDN_SETPRIO=1 -DRDN_HALF_REMAP=1", "tstag": "-DRDN_TAIL_STAG=1",
-            "tsgb1": "-DRDN_TAIL_SGB=1", "tsgb2": "-DRDN_TAIL_SGB=2", "tsgb4": "-DRDN_TAIL_SGB=4", "tsgb8": "-DRDN_TAIL_SGB=8"}
+            "tsgb1": "-DRDN_TAIL_SGB=1", "tsgb2": "-DRDN_TAIL_SGB=2", "tsgb4": "-DRDN_TAIL_SGB=4", "tsgb8": "-DRDN_TAIL_SGB=8",
+            "stgfirst": "-DRDN_STAGE_FIRST=1",
+            "tearly": "-DRDN_TAIL_EARLY=1", "tearlyhs": "-DRDN_TAIL_EARLY=1 -DRDN_HYB_STAMPS=1"}
 
 
 def build():

@@ -75,6 +75,13 @@ def main():
         c = w[1 + k] / n
         extra = f"  ({c / PER_LAYER[k]:.0f} per layer)" if k in PER_LAYER else ""
         print(f"  {name:42s} {c:9.0f} cycles  {100 * w[1 + k] / tot:5.1f} %{extra}")
+    if os.environ.get("RDN_WALK") == "1" and any(w[16:22]):
+        # wave 0's view of each corrected layer, per block (inplace.hpp conv, RDN_HYB_STAMPS)
+        blocks = w[16:22]
+        per = n * 5
+        print("  corrected layer, wave 0, per block (cycles per layer): " +
+              "  ".join(f"{'stores' if k == 5 else 'block ' + str(k)} {v / per:.0f}" for k, v in enumerate(blocks)) +
+              f"  = {sum(blocks) / per:.0f}")
 
 
 if __name__ == "__main__":
