@@ -254,7 +254,8 @@ static bool walk_tiles(int arch, int dtype, int64_t n, int64_t L, hipStream_t s)
 static int forward_impl(const char* who, int arch, int dtype, const void* packed, const float* x, float* y, int64_t n,
                         int64_t L, void* ws, size_t ws_bytes, const rdn::met::MetricOut* mo, hipStream_t s, bool* fused) {
   if (!valid_arch(arch) || !valid_dtype(dtype)) return fail(RDN_EINVAL, std::string(who) + ": unknown arch/dtype");
-  if (!packed || !x || !y) return fail(RDN_EINVAL, std::string(who) + ": null pointer");
+  // x / y may be NULL for an empty batch (an empty torch tensor's data pointer); the blob may not
+  if (!packed || (n > 0 && (!x || !y))) return fail(RDN_EINVAL, std::string(who) + ": null pointer");
   if (n < 0 || L < 1 || L > 0x7fffffff) return fail(RDN_EINVAL, std::string(who) + ": need n >= 0 and 1 <= L < 2^31");
   if (mo && L < 7) return fail(RDN_EINVAL, std::string(who) + ": need L >= 7 (SSIM window)");
   if (n == 0) return RDN_OK;
@@ -304,7 +305,7 @@ int rdn_forward_metrics(int arch, int dtype, const void* packed, const float* x,
                         const void* clean, int clean_is_f64, double* per_spectrum, double* sums, int64_t* acc, void* ws,
                         size_t ws_bytes, void* stream, int* fused) {
   RDN_GUARD_BEGIN
-  if (!clean) return fail(RDN_EINVAL, "rdn_forward_metrics: null clean pointer");
+  if (!clean && n > 0) return fail(RDN_EINVAL, "rdn_forward_metrics: null clean pointer");
   if (clean_is_f64 != 0 && clean_is_f64 != 1) return fail(RDN_EINVAL, "rdn_forward_metrics: clean_is_f64 must be 0 or 1");
   const rdn::met::MetricOut mo{clean, clean_is_f64, per_spectrum, sums, (long long*)acc};
   bool f = false;
@@ -336,7 +337,9 @@ static int forward_status(const char* who, int arch, int dtype, int64_t n, int64
     // the input-gate bit is informational (the module's fp32 re-run decision): only the range bit fails
     return rc != RDN_OK || !(w & rdn::STATUS_RANGE) ? rc : fail(RDN_ERANGE, range_msg());
   }
-  if (n == 0) return hip_check(hipStreamSynchronize(s), who);
+  // n = 0 with no workspace: nothing ran.  With one, its sticky words may hold earlier forwards' bits
+  // (a workspace made for an empty batch and reused for larger ones): read them
+  if (n == 0 && !ws) return hip_check(hipStreamSynchronize(s), who);
   const size_t need = rdn::cbam_workspace_bytes(arch, dtype, n, L, s);
   if (ws_bytes < need || (need && !ws))
     return fail(RDN_ESIZE, std::string(who) + ": workspace smaller than this device's CBAM geometry needs (" +
@@ -370,7 +373,7 @@ int rdn_forward_status_ex(int arch, int dtype, int64_t n, int64_t L, void* ws, s
 int rdn_generate(uint64_t seed, uint64_t first_index, int64_t n, const rdn_gen_params* p, float* clean, float* noisy,
                  float* snr_db, float* noise_std, void* stream) {
   RDN_GUARD_BEGIN
-  if (!p || !clean || !noisy) return fail(RDN_EINVAL, "rdn_generate: null pointer");
+  if (!p || (n > 0 && (!clean || !noisy))) return fail(RDN_EINVAL, "rdn_generate: null pointer");
   if (n < 0 || p->signal_length < 1 || p->signal_length > 0x7fffffff || p->max_repeat < 1 || !(p->snr_hi >= p->snr_lo))
     return fail(RDN_EINVAL, "rdn_generate: bad parameters");
   if (n == 0) return RDN_OK;
@@ -384,7 +387,7 @@ int rdn_generate(uint64_t seed, uint64_t first_index, int64_t n, const rdn_gen_p
 int rdn_metrics(const float* y, const float* clean, int64_t n, int64_t L, double* per_spectrum, double* sums,
                 void* stream) {
   RDN_GUARD_BEGIN
-  if (!y || !clean) return fail(RDN_EINVAL, "rdn_metrics: null pointer");
+  if (n > 0 && (!y || !clean)) return fail(RDN_EINVAL, "rdn_metrics: null pointer");
   if (n < 0 || L < 7 || L > 0x7fffffff) return fail(RDN_EINVAL, "rdn_metrics: need L >= 7 (SSIM window)");
   if (n == 0) return RDN_OK;
   return hip_check(rdn::launch_metrics(y, clean, false, n, (int)L, per_spectrum, sums, nullptr, (hipStream_t)stream),
@@ -395,7 +398,7 @@ int rdn_metrics(const float* y, const float* clean, int64_t n, int64_t L, double
 int rdn_metrics_ex(const float* y, const void* clean, int clean_is_f64, int64_t n, int64_t L, double* per_spectrum,
                    double* sums, int64_t* acc, void* stream) {
   RDN_GUARD_BEGIN
-  if (!y || !clean) return fail(RDN_EINVAL, "rdn_metrics_ex: null pointer");
+  if (n > 0 && (!y || !clean)) return fail(RDN_EINVAL, "rdn_metrics_ex: null pointer");
   if (clean_is_f64 != 0 && clean_is_f64 != 1) return fail(RDN_EINVAL, "rdn_metrics_ex: clean_is_f64 must be 0 or 1");
   if (n < 0 || L < 7 || L > 0x7fffffff) return fail(RDN_EINVAL, "rdn_metrics_ex: need L >= 7 (SSIM window)");
   if (n == 0) return RDN_OK;

@@ -163,7 +163,9 @@ int rdn_workspace_init(int arch, int dtype, int64_t n, int64_t L, void* workspac
 
 /* y[n][L] = Model(x[n][L]) on the device.  x, y: fp32 device pointers (the (N,1,L) tensor is
  * (N,L) contiguous) that must not overlap (RDN_EINVAL: tiles re-read input halos while outputs are
- * written); packed: device copy of the rdn_pack blob; stream: hipStream_t or NULL. */
+ * written); packed: device copy of the rdn_pack blob; stream: hipStream_t or NULL.  n = 0 launches
+ * nothing and returns RDN_OK; x and y may then be NULL (every entry point below that takes a batch
+ * accepts NULL data pointers for n = 0 the same way). */
 int rdn_forward(int arch, int dtype, const void* packed, const float* x, float* y, int64_t n, int64_t L,
                 void* workspace, size_t workspace_bytes, void* stream);
 
