@@ -156,6 +156,11 @@ def _check_cuda_f32(t, name):
         raise TypeError(f"{name} must be float32, got {t.dtype}")
 
 
+def _rows(t):
+    """(N, L) or (N, 1, L) -> contiguous (N, L) (N = 0 included: no -1 in the shape)."""
+    return t.reshape(t.shape[0], t.shape[-1] if t.dim() > 1 else 1).contiguous()
+
+
 def _check_out(t, name, shape, device, dtype=torch.float32):
     """A caller-supplied output buffer the kernels write through a raw pointer: it must be exactly
     the size, type and device the launch assumes, and contiguous."""
@@ -335,7 +340,7 @@ def forward_metrics(arch, dtype, packed, x, clean, out=None, sums=None, per_spec
     if clean.dtype not in (torch.float32, torch.float64):
         raise TypeError(f"clean must be float32 or float64, got {clean.dtype}")
     n, L, a, code, y, ws = _forward_args(arch, dtype, x, out, check, workspace, False)
-    clean = clean.reshape(clean.shape[0], -1).contiguous()
+    clean = _rows(clean)
     if tuple(clean.shape) != (n, L):
         raise ValueError(f"clean must be ({n}, {L}), got {tuple(clean.shape)}")
     if clean.device != x.device:
@@ -399,8 +404,8 @@ def metrics(y, clean, sums=None, per_spectrum=True, acc=None):
         raise RuntimeError("raman_mi355x runs on the GPU only: clean must be a CUDA (HIP) tensor")
     if clean.dtype not in (torch.float32, torch.float64):
         raise TypeError(f"clean must be float32 or float64, got {clean.dtype}")
-    y = y.reshape(y.shape[0], -1).contiguous()
-    clean = clean.reshape(clean.shape[0], -1).contiguous()
+    y = _rows(y)
+    clean = _rows(clean)
     if y.shape != clean.shape:
         raise ValueError(f"shape mismatch {tuple(y.shape)} vs {tuple(clean.shape)}")
     n, L = y.shape
