@@ -101,6 +101,15 @@ constexpr int BIAS_OFF = H16_BIAS_OFF;
 #ifndef RDN_H16_ESPLIT
 #define RDN_H16_ESPLIT 0
 #endif
+#ifndef RDN_PRIO_SWITCH
+// Ping-pong layers: the two waves of a SIMD (w, w + 4: the two channel halves) share its MFMA pipe, and
+// at equal priority the arbiter favours the older wave, so waves 0-3 finish a layer's MFMA stream ~1k
+// cycles before waves 4-7, which then run it alone (one wave per SIMD) up to the barrier
+// (tools/hyb_stamps.py, per-wave layer stamps).  RDN_PRIO_SWITCH = k > 0: waves 4-7 raise their
+// priority when they reach N-tile k of a layer (and drop it at the next layer's start), so that both
+// waves of a SIMD reach the barrier together
+#define RDN_PRIO_SWITCH 0
+#endif
 #ifndef RDN_H16_SGB
 #define RDN_H16_SGB 0
 #endif
@@ -169,6 +178,11 @@ struct Tile {
   int cs_cur, cs_prev, dn_prev, dnext;
   bool first;
   unsigned* status;      // the launch's status word (input gate, STATUS_GATE) or NULL
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+  // diagnostic (tools/hyb_stamps.py): the walk's ReLU layers, wave 0's view -- entry to the first MFMA
+  // issue (fill), to the last MFMA issue, to the last epilogue's store, to past the barrier; layers
+  unsigned long long lst[5];
+#endif
 };
 
 struct Frags {            // one layer's operands in VGPRs: this wave's A-fragments and folded bias
@@ -507,6 +521,9 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     cc = carry_load(tl, src, CA);
   }
   const int pos0 = tl.base + CG + rblock(w) * RW;
+#if RDN_PRIO_SWITCH
+  if (h) __builtin_amdgcn_s_setprio(0);
+#endif
 
   // Idle waves of a short last tile: every row of this wave lies at position >= L + 2, beyond the
   // reach (d <= 2) of any row that matters, so it skips the layer's MFMAs and only zeroes its dst
@@ -592,6 +609,10 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
     store_slot(p, v, valid, n);
   };
 
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+  constexpr bool LST = WALK && EPI == RELU;
+  unsigned long long lt[5] = {__builtin_amdgcn_s_memtime(), 0, 0, 0, 0};
+#endif
   Acc prev;
   constexpr int PF = RDN_H16_PF;       // B fragments in flight ahead of the step that consumes them
   constexpr int K = KS * NT;           // steps (N-tile n, k-step s), k = KS n + s
@@ -608,6 +629,9 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int k = KS * n + s, kp = k + PF;
+#if RDN_PRIO_SWITCH
+      if (n == RDN_PRIO_SWITCH && s == 0 && h) __builtin_amdgcn_s_setprio(1);
+#endif
 #if defined(RDN_ABLATE_NOLDS)
       if (kp < K) { B[kp % (PF + 1)] = B[(k + 1) % (PF + 1)]; asm volatile("" : "+v"(B[kp % (PF + 1)])); }
 #else
@@ -617,6 +641,10 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
         if (n > 0 && s == 0) idn[n & 1] = *(const V*)(tl.lds + sid + n * NR * ROWB);
       }
       mstep(F, s, B[k % (PF + 1)], acc);
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+      if (LST && k == 0) lt[1] = __builtin_amdgcn_s_memtime();
+      if (LST && k == K - 1) lt[2] = __builtin_amdgcn_s_memtime();
+#endif
       if constexpr (ESPLIT) {
         if (n > 0 && s == 1) {
           V hv = __builtin_convertvector(__builtin_shufflevector(prev.v[0], prev.v[1], 0, 1, 2, 3, 4, 5, 6, 7), V);
@@ -655,10 +683,21 @@ __device__ __forceinline__ void layer(Tile& tl, uint32_t src, uint32_t dst, int 
   // until the barrier below)
   if (WALK && walk_id) *walk_id = *(const V*)(tl.lds + src + (h ? tl.koff[2][1] : tl.koff[2][0]));
   tl.layer += 1;
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+  if (LST) lt[3] = __builtin_amdgcn_s_memtime();
+#endif
 #if defined(RDN_ABLATE_NOBARRIER)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #else
   lds_barrier();
+#endif
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+  if (LST) {
+    lt[4] = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tl.lst[k] += lt[k + 1] - lt[k];
+    tl.lst[4] += 1;
+  }
 #endif
 }
 

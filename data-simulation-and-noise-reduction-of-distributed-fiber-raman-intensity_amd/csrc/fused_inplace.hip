@@ -354,6 +354,9 @@ __device__ __forceinline__ void hybrid_walk_spectrum(char* lds, const uint8_t* _
   tl.first = true;
   hybw::PP::Tile t16 = hybw::PP::init_tile(lds, blob, blob + SMALL_BYTES, tl.x, L, 0);
   t16.status = status;
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+  for (int k = 0; k < 5; ++k) t16.lst[k] = 0;
+#endif
   hybw::PP::Frags F0, F1;
   hybw::PP::load_frags(t16, 0, F1);
   hybw::PP::StemX xs = hybw::PP::walk_stem_load(t16, 0, hybw::RIGHT_C0);
@@ -367,6 +370,10 @@ __device__ __forceinline__ void hybrid_walk_spectrum(char* lds, const uint8_t* _
   for (; t < ntiles && (t + 1) * hybw::PP::WT <= L; ++t) hybw::tile<false>(tl, t16, y, t, ntiles, F0, F1, xs, status, st);
   for (; t < ntiles; ++t) hybw::tile<true>(tl, t16, y, t, ntiles, F0, F1, xs, status, st);
   st.flush(status);
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+  if (status && (__builtin_amdgcn_workitem_id_x() & 63) == 0)      // every wave's view: words 32 + 5 w + k
+    for (int k = 0; k < 5; ++k) atomicAdd((unsigned long long*)status + 32 + 5 * (__builtin_amdgcn_workitem_id_x() >> 6) + k, t16.lst[k]);
+#endif
 }
 // MET: the spectrum's metrics follow its walk in the same workgroup (metrics.hpp walk_metrics; a
 // separate instantiation, so the plain forward's register allocation does not see the epilogue).  The

@@ -28,7 +28,9 @@ VARIANTS = {"base": "", "prev": "", "cur": "", "cur2": "", "nolds": "-DRDN_ABLAT
             "prioremap": "-DRDN_SETPRIO=1 -DRDN_HALF_REMAP=1", "tstag": "-DRDN_TAIL_STAG=1",
             "tsgb1": "-DRDN_TAIL_SGB=1", "tsgb2": "-DRDN_TAIL_SGB=2", "tsgb4": "-DRDN_TAIL_SGB=4", "tsgb8": "-DRDN_TAIL_SGB=8",
             "stgfirst": "-DRDN_STAGE_FIRST=1",
-            "tearly": "-DRDN_TAIL_EARLY=1", "tearlyhs": "-DRDN_TAIL_EARLY=1 -DRDN_HYB_STAMPS=1"}
+            "tearly": "-DRDN_TAIL_EARLY=1", "tearlyhs": "-DRDN_TAIL_EARLY=1 -DRDN_HYB_STAMPS=1",
+            "psw2": "-DRDN_PRIO_SWITCH=2", "psw3": "-DRDN_PRIO_SWITCH=3", "psw4": "-DRDN_PRIO_SWITCH=4",
+            "psw5": "-DRDN_PRIO_SWITCH=5", "psw6": "-DRDN_PRIO_SWITCH=6", "psw4hs": "-DRDN_PRIO_SWITCH=4 -DRDN_HYB_STAMPS=1"}
 
 
 def build():

@@ -51,16 +51,16 @@ def main():
     assert lib.rdn_pack(1, 5, ptrs, numels, len(host), ctypes.c_void_p(blob.data_ptr()), size.value) == 0
     blob = blob.to(dev)
     y = torch.empty_like(noisy)
-    ws = torch.zeros(256, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(1024, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
     for _ in range(3):                                  # warm-up
-        lib.rdn_forward(1, 5, blob.data_ptr(), noisy.data_ptr(), y.data_ptr(), B, L, ws.data_ptr(), 256, stream)
+        lib.rdn_forward(1, 5, blob.data_ptr(), noisy.data_ptr(), y.data_ptr(), B, L, ws.data_ptr(), 1024, stream)
     torch.cuda.synchronize()
     ws.zero_()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(5):
-        assert lib.rdn_forward(1, 5, blob.data_ptr(), noisy.data_ptr(), y.data_ptr(), B, L, ws.data_ptr(), 256, stream) == 0
+        assert lib.rdn_forward(1, 5, blob.data_ptr(), noisy.data_ptr(), y.data_ptr(), B, L, ws.data_ptr(), 1024, stream) == 0
     e1.record()
     torch.cuda.synchronize()
     w = ws.view(torch.int64).cpu().tolist()
@@ -75,6 +75,14 @@ def main():
         c = w[1 + k] / n
         extra = f"  ({c / PER_LAYER[k]:.0f} per layer)" if k in PER_LAYER else ""
         print(f"  {name:42s} {c:9.0f} cycles  {100 * w[1 + k] / tot:5.1f} %{extra}")
+    if os.environ.get("RDN_WALK") == "1" and len(w) > 72 and w[36]:
+        # every wave's view of the ping-pong ReLU layers (fused16.hpp layer, RDN_HYB_STAMPS)
+        print("  ping-pong ReLU layer per wave (cycles per layer): fill (entry -> first MFMA issue) / MFMA "
+              "stream (first -> last issue) / drain (-> last store) / barrier wait")
+        for wv in range(8):
+            q = w[32 + 5 * wv: 37 + 5 * wv]
+            nl = q[4]
+            print(f"    wave {wv}: " + " / ".join(f"{v / nl:.0f}" for v in q[:4]) + f"  = {sum(q[:4]) / nl:.0f}")
     if os.environ.get("RDN_WALK") == "1" and any(w[16:22]):
         # wave 0's view of each corrected layer, per block (inplace.hpp conv, RDN_HYB_STAMPS)
         blocks = w[16:22]
