@@ -161,3 +161,19 @@ def test_forward_metrics_spiked_spectra_take_the_epilogue(monkeypatch):
     assert torch.equal(y0, y1)
     assert torch.equal(per0, per1)
     assert sums1[4].item() == n
+
+
+@pytest.mark.parametrize("arch", ["RRCDNet", "DSDN", "ADSDN"])
+def test_evaluate_synthetic_fused_metering_same_bits(arch, monkeypatch):
+    """Config 4's driver (evaluate_synthetic) metering through the walk kernels' epilogue
+    (rdn_forward_metrics) and through forward + the metrics kernel: the same exact accumulators (the
+    per-spectrum values are the same bits, metrics.hpp), on ragged chunks (20 spectra in chunks of 8);
+    RDN_WALK=1 forces the walk geometry where it exists (ADSDN: the team kernel, never fused)."""
+    from raman_mi355x.evaluate import evaluate_synthetic
+    monkeypatch.setenv("RDN_WALK", "1")
+    m = _model(arch, "f16")
+    kw = dict(seed=SEED, signal_length=1500, batch_size=8, first_index=123)
+    fused = evaluate_synthetic({arch: m}, 20, fused_metrics=True, **kw)[arch]
+    plain = evaluate_synthetic({arch: m}, 20, fused_metrics=False, **kw)[arch]
+    assert fused["acc"] == plain["acc"] and fused["acc"][-1] == 20
+    assert fused["means"] == plain["means"]
