@@ -1048,7 +1048,11 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+#if defined(RDN_ABLATE_NOALOAD_TAIL)       // diagnostic builds only (tools/ablate.py): wrong results
+      if (has_next && load_next(j) && tl.layer < 0) {
+#else
       if (has_next && load_next(j)) {                                  // last use of a[.][s]
+#endif
 #pragma unroll
         for (int mm = 0; mm < MT; ++mm) {
           if constexpr (MODE == MODE_H8 && !LOADC) O::load_a_main(wnext, MT * mp + mm, s, lane, a[mm][s]);
