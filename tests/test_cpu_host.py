@@ -353,3 +353,19 @@ def test_team16_xcd_placement_is_a_bijection(teams, TT):
         if x is not None:
             assert wg % 8 == x and xcd.setdefault(team, x) == x
     assert len(seen) == teams * TT
+
+
+def test_row_views_and_empty_batches_on_the_host():
+    """engine._rows: (N, L) and (N, 1, L) -> contiguous (N, L), N = 0 included (no -1 in the view); and
+    the eager (reference) forward of every module on an empty CPU batch returns an empty (0, 1, L)."""
+    import raman_mi355x as R
+    from raman_mi355x import engine
+    for shape in [(3, 50), (3, 1, 50), (0, 50), (0, 1, 50)]:
+        t = torch.zeros(shape)
+        r = engine._rows(t)
+        assert tuple(r.shape) == (shape[0], 50) and r.is_contiguous()
+    x = torch.zeros((0, 1, 40))
+    for name, cls in R.MODELS.items():
+        with torch.no_grad():
+            y = cls().eval()(x)
+        assert tuple(y.shape) == (0, 1, 40), name
