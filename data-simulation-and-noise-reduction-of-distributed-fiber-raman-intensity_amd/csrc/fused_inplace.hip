@@ -356,6 +356,7 @@ __device__ __forceinline__ void hybrid_walk_spectrum(char* lds, const uint8_t* _
   t16.status = status;
 #if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
   for (int k = 0; k < 5; ++k) t16.lst[k] = 0;
+  tl.bwork = tl.bwait = 0;
 #endif
   hybw::PP::Frags F0, F1;
   hybw::PP::load_frags(t16, 0, F1);
@@ -373,6 +374,10 @@ __device__ __forceinline__ void hybrid_walk_spectrum(char* lds, const uint8_t* _
 #if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
   if (status && (__builtin_amdgcn_workitem_id_x() & 63) == 0)      // every wave's view: words 32 + 5 w + k
     for (int k = 0; k < 5; ++k) atomicAdd((unsigned long long*)status + 32 + 5 * (__builtin_amdgcn_workitem_id_x() >> 6) + k, t16.lst[k]);
+  if (status && (__builtin_amdgcn_workitem_id_x() & 63) == 0) {     // words 80 + 2 w: corrected-layer work / wait
+    atomicAdd((unsigned long long*)status + 80 + 2 * (__builtin_amdgcn_workitem_id_x() >> 6), tl.bwork);
+    atomicAdd((unsigned long long*)status + 81 + 2 * (__builtin_amdgcn_workitem_id_x() >> 6), tl.bwait);
+  }
 #endif
 }
 // MET: the spectrum's metrics follow its walk in the same workgroup (metrics.hpp walk_metrics; a

@@ -100,6 +100,11 @@ struct Tile {
   // and its carry rows' dilation, the dilation of the layer reading this one, first tile of a spectrum
   int cs_cur, cs_prev, dn_prev, dnext;
   bool first;
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+  // diagnostic (tools/hyb_stamps.py): this wave's cycles working / waiting at the corrected walk layers'
+  // block barriers (flushed once per spectrum by rrcdnet_hybrid_walk)
+  unsigned long long bwork, bwait;
+#endif
 };
 
 __device__ __forceinline__ bool in_range(int p, int L) { return p >= 0 && p < L; }
@@ -1101,22 +1106,42 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
         }
         res[j][i][mm] = v;
       }
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+    const unsigned long long pre_b = __builtin_amdgcn_s_memtime();
+#endif
 #if defined(RDN_ABLATE_NOBARRIER)         // diagnostic builds only (tools/ablate.py): wrong results
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #else
     lds_barrier();                 // every wave is done reading the rows block j needed
 #endif
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+    if (WALK && MODE == MODE_H8) {
+      const unsigned long long post_b = __builtin_amdgcn_s_memtime();
+      tl.bwork += pre_b - bst_t;
+      tl.bwait += post_b - pre_b;
+    }
+#endif
     bstamp(j);
   }
   store_block(NB - 2);
   store_block(NB - 1);
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+  const unsigned long long pre_s = __builtin_amdgcn_s_memtime();
+#endif
   lds_barrier();                   // the layer's output is complete
+#if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
+  if (WALK && MODE == MODE_H8) {
+    tl.bwork += pre_s - bst_t;
+    tl.bwait += __builtin_amdgcn_s_memtime() - pre_s;
+  }
+#endif
   bstamp(NB);
 #if defined(RDN_HYB_STAMPS) && RDN_HYB_STAMPS
   if (WALK && MODE == MODE_H8 && tl.status && tid == 0) {
 #pragma unroll
     for (int k = 0; k <= NB; ++k) atomicAdd((unsigned long long*)tl.status + 16 + k, bst[k]);
   }
+
 #endif
   tl.layer += 1;
   if constexpr (WALK) {

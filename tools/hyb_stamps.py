@@ -83,6 +83,11 @@ def main():
             q = w[32 + 5 * wv: 37 + 5 * wv]
             nl = q[4]
             print(f"    wave {wv}: " + " / ".join(f"{v / nl:.0f}" for v in q[:4]) + f"  = {sum(q[:4]) / nl:.0f}")
+    if os.environ.get("RDN_WALK") == "1" and len(w) > 95 and w[80]:
+        # every wave's cycles working / waiting at the corrected walk layers' block barriers
+        print("  corrected layer per wave (cycles per layer): working / waiting at block barriers")
+        for wv in range(8):
+            print(f"    wave {wv}: {w[80 + 2 * wv] / (n * 5):.0f} / {w[81 + 2 * wv] / (n * 5):.0f}")
     if os.environ.get("RDN_WALK") == "1" and any(w[16:22]):
         # wave 0's view of each corrected layer, per block (inplace.hpp conv, RDN_HYB_STAMPS)
         blocks = w[16:22]
