@@ -50,8 +50,12 @@ template <int NBK> struct TileGeo {
 #ifndef RDN_HALF_REMAP
 #define RDN_HALF_REMAP 0
 #endif
+#ifndef RDN_TAIL_SWAP
+#define RDN_TAIL_SWAP 0       // A/B: the half block on waves 4-7 instead of 0-3 (inplace.hpp conv)
+#endif
 #ifndef RDN_TAIL_EARLY
 #define RDN_TAIL_EARLY 0      // A/B: next-layer operand loads of the half block's idle waves one block early
+                              // (1: all; 2: the fragments, bias and scales at the last block; 3: k-step 0 only)
 #endif
 #ifndef RDN_STAGE_FIRST
 #define RDN_STAGE_FIRST 0     // A/B (the hybrid walk): layer 9's plane stores before the tail's operand loads
@@ -775,7 +779,13 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   // of 16: same swizzle, one address add per access), so the half block costs half a block
   constexpr bool REMAP = TG::HALF && RDN_HALF_REMAP;
   static_assert(!REMAP || MODE == MODE_H8, "the half-block remap is written for the f16 + e4m3 write-back");
-  const bool half_idle = TG::HALF && !REMAP && (__builtin_amdgcn_readfirstlane(tid >> 6) >> 1) >= 2;
+  // RDN_TAIL_SWAP: the half block's rows go to the waves of quarters 2-3 (4-7: the younger wave of each
+  // SIMD, which finishes the full blocks last), shifted down by 64 rows, and waves 0-3 idle there instead
+  // -- with RDN_TAIL_EARLY those fetch the next layer's operands in block NB - 2, where they have slack
+  constexpr bool SWAP = TG::HALF && !REMAP && RDN_TAIL_SWAP;
+  const bool half_idle = TG::HALF && !REMAP && ((__builtin_amdgcn_readfirstlane(tid >> 6) >> 1) >= 2) != SWAP;
+  const uint32_t hsw = SWAP && (__builtin_amdgcn_readfirstlane(tid >> 6) >> 1) >= 2 ? 64u * ROWB_F32 : 0u;
+  auto swapped = [&](int j) { return SWAP && j == NB - 1; };
   const bool stag_late = RDN_TAIL_STAG && __builtin_amdgcn_readfirstlane(tid >> 6) >= 4;
   constexpr bool SGB = RDN_TAIL_SGB && !RDN_TAIL_STAG && MODE == MODE_H8 && cin && !(EPI & (ADD_ID | SAVE_ID));
   const uint32_t hoff = REMAP ? (uint32_t)(16 * ROWB_F32) * (uint32_t)__builtin_amdgcn_readfirstlane(nq) : 0u;
@@ -838,6 +848,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
     if (TG::WRAP && j == 0 && s < TS && i == 0) return ldb(bfirst[s], 0);
     if (TG::WRAP && j == NB - 1 && s >= 2 * TS && i == NT - 1) return ldb(blast[s - 2 * TS], 0);
     if (remapped(j)) return ldb(j >= 2 ? badr2[s] : badr[s], (uint32_t)(BR * (j >= 2 ? j - 2 : j)) * ROWB_F32 - hoff);
+    if (swapped(j)) return ldb(badr2[s], (uint32_t)(BR * (j - 2) + 16 * i) * ROWB_F32 - hsw);
     if (j >= 2) return ldb(badr2[s], (uint32_t)(BR * (j - 2) + 16 * i) * ROWB_F32);
     return ldb(badr[s], (uint32_t)(BR * j + 16 * i) * ROWB_F32);
   };
@@ -886,7 +897,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
   // stores instead of 6); ReLU folded into the saturating med3
   auto store_pair = [&](int j, int i) {
     if constexpr (MODE == MODE_H8) {                // (instantiated in every mode, called in MODE_H8)
-      const int rb = BR * j + (remapped(j) ? 16 : BR / 4) * nq;
+      const int rb = BR * j + (remapped(j) ? 16 : BR / 4) * nq - (swapped(j) ? 64 : 0);
       const bool inside = !EDGE || (tl.base + rb >= 0 && tl.base + rb + (remapped(j) ? 16 : BR / 4) <= tl.L);
       const bool zero = !inside && !in_range(tl.base + rb + 16 * i + c16, tl.L);
       if (!cout) {                 // plain f16 output (the next layer is uncorrected): no e4m3 planes
@@ -900,7 +911,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
           if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
           hv[mm] = __builtin_convertvector(v, f16x4);
         }
-        *(f16x8*)(tl.lds + sadr[0][0] + (uint32_t)(BR * j + 16 * i) * ROWB_F32 - (remapped(j) ? hoff : 0u)) =
+        *(f16x8*)(tl.lds + sadr[0][0] + (uint32_t)(BR * j + 16 * i) * ROWB_F32 - (remapped(j) ? hoff : 0u) - (swapped(j) ? hsw : 0u)) =
             __builtin_shufflevector(hv[0], hv[1], 0, 1, 2, 3, 4, 5, 6, 7);
         return;
       }
@@ -915,7 +926,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
         if (EPI & SAVE_ID) id[(j * NT + i) * MT + mm] = v;
         x[mm] = h8_split(v);
       }
-      const uint32_t off = (uint32_t)(BR * j + 16 * i) * ROWB_F32 - (remapped(j) ? hoff : 0u);
+      const uint32_t off = (uint32_t)(BR * j + 16 * i) * ROWB_F32 - (remapped(j) ? hoff : 0u) - (swapped(j) ? hsw : 0u);
       typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   #if defined(RDN_ABLATE_NOSTORE)
       if (x[0].hi8 == 0x12345678u)
@@ -978,7 +989,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #pragma unroll
         for (int mm = 0; mm < MT; ++mm) hi[i][mm] = bias_l[mm];
     }
-    if (has_next && load_next(j)) {                   // last use of this layer's bias
+    if (has_next && (RDN_TAIL_EARLY >= 2 ? j == NB - 1 : load_next(j))) {   // last use of this layer's bias
 #pragma unroll
       for (int mm = 0; mm < MT; ++mm) a.bias[mm] = load_bias<MODE>(wnext, MT * mp + mm), a.sc[mm] = load_scale<MODE>(wnext, MT * mp + mm);
     }
@@ -1056,7 +1067,7 @@ __device__ __forceinline__ void conv(Tile& tl, int dil, f32x4 (&id)[16 * NBK / 4
 #if defined(RDN_ABLATE_NOALOAD_TAIL)       // diagnostic builds only (tools/ablate.py): wrong results
       if (has_next && load_next(j) && tl.layer < 0) {
 #else
-      if (has_next && load_next(j)) {                                  // last use of a[.][s]
+      if (has_next && (RDN_TAIL_EARLY == 3 && s > 0 ? j == NB - 1 : load_next(j))) {   // last use of a[.][s]
 #endif
 #pragma unroll
         for (int mm = 0; mm < MT; ++mm) {

@@ -31,7 +31,10 @@ VARIANTS = {"base": "", "prev": "", "cur": "", "cur2": "", "nolds": "-DRDN_ABLAT
             "tearly": "-DRDN_TAIL_EARLY=1", "tearlyhs": "-DRDN_TAIL_EARLY=1 -DRDN_HYB_STAMPS=1",
             "psw2": "-DRDN_PRIO_SWITCH=2", "psw3": "-DRDN_PRIO_SWITCH=3", "psw4": "-DRDN_PRIO_SWITCH=4",
             "psw5": "-DRDN_PRIO_SWITCH=5", "psw6": "-DRDN_PRIO_SWITCH=6", "psw4hs": "-DRDN_PRIO_SWITCH=4 -DRDN_HYB_STAMPS=1",
-            "tnoaload": "-DRDN_ABLATE_NOALOAD_TAIL", "tnoaloadhs": "-DRDN_ABLATE_NOALOAD_TAIL -DRDN_HYB_STAMPS=1"}
+            "tnoaload": "-DRDN_ABLATE_NOALOAD_TAIL", "tnoaloadhs": "-DRDN_ABLATE_NOALOAD_TAIL -DRDN_HYB_STAMPS=1",
+            "tswap": "-DRDN_TAIL_SWAP=1", "tswapearly": "-DRDN_TAIL_SWAP=1 -DRDN_TAIL_EARLY=1",
+            "tswapearlyhs": "-DRDN_TAIL_SWAP=1 -DRDN_TAIL_EARLY=1 -DRDN_HYB_STAMPS=1",
+            "tswape2": "-DRDN_TAIL_SWAP=1 -DRDN_TAIL_EARLY=2", "tswape3": "-DRDN_TAIL_SWAP=1 -DRDN_TAIL_EARLY=3"}
 
 
 def build():
